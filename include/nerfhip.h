@@ -1,0 +1,135 @@
+/*
+ * nerfhip.h — C ABI of the MI355X (gfx950) SIREN KV-fit engine.
+ *
+ * Drop-in boundary for the reference hot path `nerf_attention.siren.fit_siren`
+ * (reference: nerf_attention/siren.py:70-149) and its sweep driver
+ * `nerf_attention.fit.fit_kv_cache` (nerf_attention/fit.py:20-92).  The
+ * reference is pure Python and has no FFI; these entry points are what a
+ * ctypes / torch.library binding of that path binds.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Every buffer is caller-allocated DEVICE
+ *     memory (the caller owns it; the library never allocates, frees or
+ *     synchronises).  All work is enqueued on `stream` (a hipStream_t passed
+ *     as void*, NULL = default stream) and returns immediately.
+ *   - Return value: NERFHIP_OK (0) or a negative nerfhip_status.
+ *   - No global mutable state; reentrant across streams and devices.
+ *   - fp32 everywhere on the device (the reference trains in fp32,
+ *     siren.py:82-105); host-side float64 scalars (LR schedule, Adam bias
+ *     corrections) arrive pre-rounded to fp32 in `sched`.
+ *
+ * One call trains a GROUP of independent fits that share (W, D, N, epochs):
+ * each fit f has its own hidden_layers L_f <= L_max and omega_0 (so medium,
+ * deep, hifreq and lofreq — all W=256 — share one group).
+ */
+#ifndef NERFHIP_H
+#define NERFHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NERFHIP_ABI_VERSION 1
+
+typedef enum nerfhip_status {
+  NERFHIP_OK = 0,
+  NERFHIP_ERR_BAD_WIDTH = -1,      /* hidden_features not in {64,128,256,512}      */
+  NERFHIP_ERR_BAD_HEAD_DIM = -2,   /* d_head not in {64,128}                       */
+  NERFHIP_ERR_BAD_LAYERS = -3,     /* hidden_layers not in [1, NERFHIP_MAX_LAYERS]  */
+  NERFHIP_ERR_BAD_SHAPE = -4,      /* seq_len < 2, n_fits < 1, epochs < 0 ...      */
+  NERFHIP_ERR_NULL = -5,           /* a required pointer is NULL                   */
+  NERFHIP_ERR_LAUNCH = -6          /* hipGetLastError() after a launch             */
+} nerfhip_status;
+
+#define NERFHIP_MAX_LAYERS 4
+
+/* Sizes (in fp32 elements, per fit unless noted) of every buffer a group
+ * needs.  Filled by nerfhip_group_sizes(); the caller allocates
+ * n_fits * <per-fit size> for the per-fit buffers. */
+typedef struct nerfhip_sizes {
+  int64_t n_pad;           /* seq_len rounded up to the 64-row tile           */
+  int64_t params;          /* P(L_max) = 2W + L(W^2+W) + W*D + D  (state_dict order) */
+  int64_t params_t;        /* transposed weight copies: L_max*W^2 + W*D       */
+  int64_t scratch;         /* activations / grads / cos, feature-major        */
+  int64_t target;          /* n_pad * D                                       */
+  int64_t stats;           /* D (mean) — std has the same size                */
+  int64_t loss_partial;    /* epochs * n_pad/16                               */
+  int64_t rows;            /* n_pad (row_cos / row_sq)                        */
+} nerfhip_sizes;
+
+/* One group of fits.  "[n]" = per fit, strided by the matching nerfhip_sizes
+ * field; all pointers are device pointers unless marked (host). */
+typedef struct nerfhip_group {
+  int32_t W;               /* hidden_features                                 */
+  int32_t D;               /* d_head = out_features                            */
+  int32_t N;               /* seq_len                                         */
+  int32_t n_fits;
+  int32_t L_max;           /* max hidden_layers over the group                 */
+  int32_t epochs;
+  int32_t log_every;       /* probe period (siren.py:107); 0 = no probes       */
+  int32_t device;          /* HIP device ordinal the buffers and stream live on */
+
+  const int32_t* fit_layers;  /* [n_fits] hidden_layers per fit              */
+  const float* fit_omega;     /* [n_fits] omega_0 per fit                    */
+  const float* positions;     /* [n_pad] linspace(0,1,N), zero padded (siren.py:82) */
+  const float* target;        /* [n] raw KV rows [n_pad][D] (padded rows 0)  */
+  float* target_norm;         /* [n] out: (y-mean)/std   (siren.py:85-87)     */
+  float* mean;                /* [n] out: column mean [D]                      */
+  float* std;                 /* [n] out: column std (unbiased, >=1e-3) [D]    */
+  float* params;              /* [n] in: init, out: trained (state_dict order) */
+  float* params_t;            /* [n] workspace: transposed weight copies       */
+  float* adam_m;              /* [n] workspace (zeroed by the call)            */
+  float* adam_v;              /* [n] workspace (zeroed by the call)            */
+  float* scratch;             /* [n] workspace                                 */
+  const float* sched;         /* [epochs][2]: {lr_e / (1-b1^t), sqrt(1-b2^t)}  */
+  float* loss_partial;        /* [n] out: per-epoch partial sum of squared err */
+  float* probe_y;             /* [n][epochs/log_every][n_pad][D] out or NULL   */
+  float* eval_y;              /* [n] out: final normalised prediction [n_pad][D] */
+  float* row_cos;             /* [n] out: final per-row cosine  [n_pad]        */
+  float* row_sq;              /* [n] out: final per-row sum (pred-y)^2 [n_pad] */
+  float* probe_row_cos;       /* [n][epochs/log_every][n_pad] or NULL          */
+  float* probe_row_sq;        /* [n][epochs/log_every][n_pad] or NULL          */
+} nerfhip_group;
+
+int nerfhip_abi_version(void);
+const char* nerfhip_status_string(int status);
+
+/* Validate (W, D, N, L_max, epochs) and fill *out. */
+int nerfhip_group_sizes(int32_t W, int32_t D, int32_t N, int32_t L_max, int32_t epochs,
+                        nerfhip_sizes* out);
+
+/* Whole fit for every member of `n_groups` groups: prologue (normalise,
+ * transposed weights, zero Adam state), `epochs` fused train steps (forward,
+ * MSE, backward, Adam, cosine-annealed LR; siren.py:98-105), the log probes
+ * (siren.py:107-115) and the final evaluation (siren.py:119-125).
+ * Group i runs on streams[i] (a hipStream_t of device groups[i].device).
+ * Launches are interleaved epoch by epoch across the groups so that every
+ * stream has work queued and the groups run concurrently.  All groups are
+ * validated before anything is enqueued. */
+int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const* streams);
+
+/* Per-kernel device time of one group, measured with hipEvents bracketing
+ * every launch of its two step kernels (bench.py's roofline leg). */
+typedef struct nerfhip_timing {
+  int32_t group;           /* in: index of the group to time                  */
+  int32_t launches;        /* out: timed launches per kernel (= its epochs)   */
+  double rows_ms;          /* out: Σ duration of the row-step launches        */
+  double params_ms;        /* out: Σ duration of the parameter-step launches  */
+} nerfhip_timing;
+
+/* nerfhip_siren_fit + timing of group timing->group.  Unlike the untimed
+ * call it synchronises that group's stream before returning. */
+int nerfhip_siren_fit_timed(const nerfhip_group* groups, int32_t n_groups,
+                            void* const* streams, nerfhip_timing* timing);
+
+/* Forward only with the current params → eval_y (+ row metrics when
+ * target/mean/std/row_cos/row_sq are set).  SIREN.forward, siren.py:60-61. */
+int nerfhip_siren_forward(const nerfhip_group* g, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NERFHIP_H */

@@ -1,0 +1,875 @@
+// nerfhip.hip — MI355X (gfx950 / CDNA4) SIREN KV-fit engine.
+//
+// Replaces the per-epoch eager-PyTorch sequence of the reference training loop
+// (nerf_attention/siren.py:98-105: zero_grad → SIREN.forward → F.mse_loss →
+// backward → Adam.step → CosineAnnealingLR.step) with two hand-written kernels
+// per epoch, for a whole GROUP of independent fits at once:
+//
+//   k_step_rows<W,D>    row-parallel: forward (sin(ω·(xWᵀ+b)), siren.py:33-34),
+//                       MSE + dL/dŷ, backward dX chain; writes the activations
+//                       Hᵢᵀ and pre-activation grads dZᵢᵀ (feature-major) that
+//                       the weight gradients need.  One workgroup = 64 rows of
+//                       one fit; one wave = 16 rows; every GEMM on the f32 MFMA
+//                       v_mfma_f32_16x16x4_f32 in the "transposed" orientation
+//                       (Zᵀ = W·Hᵀ) so each layer's accumulator IS the next
+//                       layer's B operand (no LDS round trip, no shuffles).
+//   k_step_params<W,D>  parameter-parallel: one workgroup per 64×64 tile of
+//                       dWᵢ = dZᵢᵀ·Hᵢ₋₁ (K = seq_len, v_mfma_f32_32x32x2_f32),
+//                       bias sums, then the Adam update of that tile
+//                       (torch single-tensor Adam order, TORCH/optim/adam.py
+//                       :457-547) writing both the canonical [out][in] weights
+//                       and the transposed [in][out] copy the backward reads.
+//
+// The reduction over seq_len therefore happens inside one workgroup: no
+// partial-gradient slabs, no atomics, fully deterministic.
+//
+// Scratch layout per fit (fp32, n_pad = seq_len rounded up to 64):
+//   H_i^T  [L_max+1][W][n_pad]   activations (input of linear layer i+1)
+//   dZ_i^T [L_max+1][W][n_pad]   grad at the pre-activation of sine layer i
+//   G^T    [D][n_pad]            grad at the output (2(ŷ−y)/(N·D))
+//   cos_i  [L_max+1][n_pad/16][W/16][64][4]  cos(ω z), MFMA-fragment order
+//
+// Numerics: all fp32, inline ≈1-ulp sincos, f32-input MFMA = exact k-ordered
+// fmaf chain.  Parity target: per-fit final cosine within 1e-3 of the
+// reference PyTorch CPU path (BASELINE.json north_star).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "nerfhip.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int kRowsPerBlock = 64;   // 4 waves × 16 rows
+constexpr int kThreads = 256;
+
+struct KArgs {
+  int32_t W, D, N, n_pad, n_fits, L_max, epochs, epoch, mode;
+  int64_t p_stride, pt_stride, s_stride, t_stride, lp_stride, y_stride;
+  const int32_t* fit_layers;
+  const float* fit_omega;
+  const float* pos;
+  const float* target;
+  float* tnorm;
+  float* mean;
+  float* stdv;
+  float* params;
+  float* params_t;
+  float* m;
+  float* v;
+  float* scratch;
+  const float* sched;
+  float* loss_partial;
+  float* y_out;
+  float grad_scale;
+};
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+__device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// sin and cos of one fp32 argument (torch.sin in the forward, its derivative
+// cos in the backward, siren.py:34).  Cody–Waite reduction by π/2 with a
+// 3-term fma split (exact quotient for |x| < 2^17, far beyond the |ω·z| ≲ 10²
+// a SIREN sees), then minimax polynomials on [−π/4, π/4] (≈1 ulp, the same
+// class as the SLEEF kernels ATen uses on CPU).  Kept branch-free and short:
+// the OCML sincosf carries a Payne–Hanek path whose registers spill the
+// W ≥ 256 step kernels.
+__device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out) {
+  const float n = __builtin_rintf(x * 0.636619772367581343f);
+  float r = fmaf(n, -1.57079601287841796875f, x);
+  r = fmaf(n, -3.13916912752797361463e-07f, r);
+  r = fmaf(n, -5.39030252995776476554e-15f, r);
+  const int q = (int)n;
+  const float r2 = r * r;
+  float ps = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = fmaf(r2, ps, -1.6666654611e-1f);
+  ps = fmaf(r2 * r, ps, r);
+  float pc = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = fmaf(r2, pc, 4.166664568298827e-2f);
+  pc = fmaf(r2 * r2, pc, fmaf(r2, -0.5f, 1.0f));
+  const bool swap = q & 1;
+  float s = swap ? pc : ps;
+  float c = swap ? ps : pc;
+  s = (q & 2) ? -s : s;
+  c = ((q + 1) & 2) ? -c : c;
+  *s_out = s;
+  *c_out = c;
+}
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// XCD-aware block → (fit, tile).  Blocks b and b+8 share an XCD (observed
+// round-robin dispatch, MI355X_MICROARCH.md §Workgroup dispatch); every tile
+// of a fit goes to the same b%8 class so its weights and scratch stay in one
+// XCD's L2.  Speed only — correctness never depends on placement.
+__device__ __forceinline__ bool map_block(int b, int n_fits, int n_tiles, int& fit, int& tile) {
+  const int x = b & 7, idx = b >> 3;
+  const int slot = idx / n_tiles;
+  tile = idx - slot * n_tiles;
+  fit = x + 8 * slot;
+  return fit < n_fits;
+}
+
+__host__ __device__ inline int64_t off_hidden_w(int W, int i) {  // i = 1..L
+  return 2 * (int64_t)W + (int64_t)(i - 1) * ((int64_t)W * W + W);
+}
+__host__ __device__ inline int64_t off_final_w(int W, int L) {
+  return 2 * (int64_t)W + (int64_t)L * ((int64_t)W * W + W);
+}
+__host__ __device__ inline int64_t n_params(int W, int D, int L) {
+  return off_final_w(W, L) + (int64_t)W * D + D;
+}
+
+// torch.optim.Adam, single-tensor path (the reference runs on CPU, where the
+// foreach/fused paths are unavailable): TORCH/optim/adam.py:457,476,531-547.
+__device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g,
+                                            float step_size, float bc2_sqrt) {
+  m = m + 0.1f * (g - m);                        // exp_avg.lerp_(grad, 1-β1)
+  v = v * 0.999f;                                // exp_avg_sq.mul_(β2)
+  v = v + (0.001f * g) * g;                      //   .addcmul_(grad, grad, 1-β2)
+  const float denom = sqrtf(v) / bc2_sqrt + 1e-8f;  // (√v / √bc2).add_(eps)
+  p = p + (-step_size) * (m / denom);            // addcdiv_(m, denom, -lr/bc1)
+}
+
+// ---------------------------------------------------------------------------
+// Row-parallel step: forward + loss + backward dX chain for 64 rows of a fit.
+// mode 0 = train step; mode 1 = forward only (writes ŷ to y_out).
+// ---------------------------------------------------------------------------
+template <int W, int D>
+__global__ void __launch_bounds__(kThreads, (W >= 256 ? 1 : 2)) k_step_rows(KArgs a) {
+  constexpr int JW = W / 16, JD = D / 16;
+  int fit, tile;
+  if (!map_block(blockIdx.x, a.n_fits, a.n_pad / kRowsPerBlock, fit, tile)) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int L = a.fit_layers[fit];
+  const float om = a.fit_omega[fit];
+  const int n_pad = a.n_pad;
+  const int rblk = tile * 4 + wave;           // 16-row block
+  const int r = rblk * 16 + c;                // this lane's row (B/D column)
+  const bool valid = r < a.N;
+  const bool train = a.mode == 0;
+
+  const float* P = a.params + fit * a.p_stride;
+  const float* PT = a.params_t + fit * a.pt_stride;
+  float* S = a.scratch + fit * a.s_stride;
+  const int64_t WN = (int64_t)W * n_pad;
+  float* SH = S;
+  float* SZ = S + (int64_t)(a.L_max + 1) * WN;
+  float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
+  float* SC = SG + (int64_t)D * n_pad;
+
+  float hp[JW][4], hc[JW][4];
+
+  // ---- layer 0: SineLayer(1, W, is_first) — K = 1, an outer product (VALU)
+  {
+    const float x = a.pos[r];
+    const float* w0 = P;
+    const float* b0 = P + W;
+#pragma unroll
+    for (int J = 0; J < JW; ++J) {
+      const f4 w = ld4(w0 + 16 * J + 4 * g), b = ld4(b0 + 16 * J + 4 * g);
+      f4 cs;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float z = __fadd_rn(__fmul_rn(x, w[q]), b[q]);
+        float s, co;
+        sincos_fast(__fmul_rn(om, z), &s, &co);
+        hp[J][q] = s;
+        cs[q] = co;
+      }
+      if (train) {
+        st4(SC + ((int64_t)rblk * JW + J) * 256 + lane * 4, cs);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) SH[(int64_t)(16 * J + 4 * g + q) * n_pad + r] = hp[J][q];
+      }
+    }
+  }
+
+  // ---- hidden SineLayers 1..L: Zᵀ = Wᵢ·Hᵀ (+b), H = sin(ω Z)
+  for (int i = 1; i <= L; ++i) {
+    const float* Wi = P + off_hidden_w(W, i);
+    const float* bi = Wi + W * W;
+#pragma unroll
+    for (int J = 0; J < JW; ++J) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = Wi + (16 * J + c) * W + 4 * g;
+#pragma unroll
+      for (int kt = 0; kt < JW; ++kt) {
+        const f4 wa = ld4(wrow + 16 * kt);
+        acc = mfma16(wa[0], hp[kt][0], acc);
+        acc = mfma16(wa[1], hp[kt][1], acc);
+        acc = mfma16(wa[2], hp[kt][2], acc);
+        acc = mfma16(wa[3], hp[kt][3], acc);
+      }
+      const f4 b = ld4(bi + 16 * J + 4 * g);
+      f4 cs;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float z = __fadd_rn(acc[q], b[q]);
+        float s, co;
+        sincos_fast(__fmul_rn(om, z), &s, &co);
+        hc[J][q] = s;
+        cs[q] = co;
+      }
+      if (train) {
+        st4(SC + (int64_t)i * WN + ((int64_t)rblk * JW + J) * 256 + lane * 4, cs);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          SH[(int64_t)i * WN + (int64_t)(16 * J + 4 * g + q) * n_pad + r] = hc[J][q];
+      }
+    }
+#pragma unroll
+    for (int J = 0; J < JW; ++J)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hp[J][q] = hc[J][q];
+  }
+
+  // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f
+  const float* Wf = P + off_final_w(W, L);
+  const float* bfp = Wf + W * D;
+  f4 y[JD];
+#pragma unroll
+  for (int J = 0; J < JD; ++J) {
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wrow = Wf + (16 * J + c) * W + 4 * g;
+#pragma unroll
+    for (int kt = 0; kt < JW; ++kt) {
+      const f4 wa = ld4(wrow + 16 * kt);
+      acc = mfma16(wa[0], hp[kt][0], acc);
+      acc = mfma16(wa[1], hp[kt][1], acc);
+      acc = mfma16(wa[2], hp[kt][2], acc);
+      acc = mfma16(wa[3], hp[kt][3], acc);
+    }
+    const f4 b = ld4(bfp + 16 * J + 4 * g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[J][q] = __fadd_rn(acc[q], b[q]);
+  }
+  if (a.y_out) {
+    float* yo = a.y_out + fit * a.y_stride + (int64_t)r * D;
+#pragma unroll
+    for (int J = 0; J < JD; ++J) {
+      // lane holds ŷ[r][16J+4g+q]: one 16-B store per J
+      st4(yo + 16 * J + 4 * g, y[J]);
+    }
+  }
+  if (!train) return;
+
+  // ---- MSE (F.mse_loss, reduction mean) and its gradient 2(ŷ−y)/numel
+  {
+    const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D;
+    float sq = 0.f;
+#pragma unroll
+    for (int J = 0; J < JD; ++J) {
+      const f4 t = ld4(T + 16 * J + 4 * g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float diff = y[J][q] - t[q];
+        sq = valid ? fmaf(diff, diff, sq) : sq;
+        const float gr = valid ? a.grad_scale * diff : 0.f;
+        y[J][q] = gr;
+        SG[(int64_t)(16 * J + 4 * g + q) * n_pad + r] = gr;
+      }
+    }
+    sq = wave_sum(sq);
+    if (lane == 0)
+      a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] = sq;
+  }
+
+  // ---- backward: dH_Lᵀ = W_fᵀ·Gᵀ
+  float dh[JW][4];
+  {
+    const float* WfT = PT + (int64_t)L * W * W;  // [W][D]
+#pragma unroll
+    for (int K = 0; K < JW; ++K) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = WfT + (16 * K + c) * D + 4 * g;
+#pragma unroll
+      for (int J = 0; J < JD; ++J) {
+        const f4 wa = ld4(wrow + 16 * J);
+        acc = mfma16(wa[0], y[J][0], acc);
+        acc = mfma16(wa[1], y[J][1], acc);
+        acc = mfma16(wa[2], y[J][2], acc);
+        acc = mfma16(wa[3], y[J][3], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dh[K][q] = acc[q];
+    }
+  }
+
+  // ---- sine layers L..0: dZ = (dH ⊙ cos(ωz))·ω ; dH_prevᵀ = Wᵢᵀ·dZᵀ
+  for (int i = L; i >= 0; --i) {
+    const float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
+    float* SZi = SZ + (int64_t)i * WN;
+#pragma unroll
+    for (int K = 0; K < JW; ++K) {
+      const f4 cs = ld4(SCi + K * 256);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float dz = __fmul_rn(__fmul_rn(dh[K][q], cs[q]), om);
+        hc[K][q] = dz;
+        SZi[(int64_t)(16 * K + 4 * g + q) * n_pad + r] = dz;
+      }
+    }
+    if (i == 0) break;
+    const float* WiT = PT + (int64_t)(i - 1) * W * W;  // [W_in][W_out]
+#pragma unroll
+    for (int K = 0; K < JW; ++K) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = WiT + (16 * K + c) * W + 4 * g;
+#pragma unroll
+      for (int J = 0; J < JW; ++J) {
+        const f4 wa = ld4(wrow + 16 * J);
+        acc = mfma16(wa[0], hc[J][0], acc);
+        acc = mfma16(wa[1], hc[J][1], acc);
+        acc = mfma16(wa[2], hc[J][2], acc);
+        acc = mfma16(wa[3], hc[J][3], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dh[K][q] = acc[q];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Parameter-parallel step: weight/bias gradients reduced over all rows, then
+// Adam.  Tiles per fit: L·(W/64)² hidden + (D/64)(W/64) final + W/64 first.
+// ---------------------------------------------------------------------------
+template <int W, int D>
+__global__ void __launch_bounds__(kThreads) k_step_params(KArgs a) {
+  constexpr int WT = W / 64;
+  constexpr int TH = WT * WT, TF = (D / 64) * WT, T0 = WT;
+  const int n_tiles_max = a.L_max * TH + TF + T0;
+  int fit, t;
+  if (!map_block(blockIdx.x, a.n_fits, n_tiles_max, fit, t)) return;
+  const int L = a.fit_layers[fit];
+  if (t >= L * TH + TF + T0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n_pad = a.n_pad;
+  const float step_size = a.sched[2 * a.epoch], bc2s = a.sched[2 * a.epoch + 1];
+
+  float* P = a.params + fit * a.p_stride;
+  float* PT = a.params_t + fit * a.pt_stride;
+  float* M = a.m + fit * a.p_stride;
+  float* V = a.v + fit * a.p_stride;
+  const float* S = a.scratch + fit * a.s_stride;
+  const int64_t WN = (int64_t)W * n_pad;
+  const float* SH = S;
+  const float* SZ = S + (int64_t)(a.L_max + 1) * WN;
+  const float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
+
+  if (t < L * TH + TF) {
+    const float *Asrc, *Bsrc;
+    int out_dim, tj, tk;
+    int64_t pw, pb, ptw;
+    if (t < L * TH) {
+      const int layer = t / TH + 1, u = t % TH;
+      tj = u / WT; tk = u % WT;
+      Asrc = SZ + (int64_t)layer * WN;
+      Bsrc = SH + (int64_t)(layer - 1) * WN;
+      out_dim = W;
+      pw = off_hidden_w(W, layer);
+      pb = pw + (int64_t)W * W;
+      ptw = (int64_t)(layer - 1) * W * W;
+    } else {
+      const int u = t - L * TH;
+      tj = u / WT; tk = u % WT;
+      Asrc = SG;
+      Bsrc = SH + (int64_t)L * WN;
+      out_dim = D;
+      pw = off_final_w(W, L);
+      pb = pw + (int64_t)W * D;
+      ptw = (int64_t)L * W * W;
+    }
+    const int wj = wave >> 1, wk = wave & 1;
+    const int h = lane >> 5, lr = lane & 31;
+    const int jrow0 = tj * 64 + wj * 32;
+    const int kcol = tk * 64 + wk * 32 + lr;
+    const float* ap = Asrc + (int64_t)(jrow0 + lr) * n_pad + 4 * h;
+    const float* bp = Bsrc + (int64_t)kcol * n_pad + 4 * h;
+    f16v acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    float bsum = 0.f;
+    const bool do_bias = (tk == 0) && (wk == 0);
+    f4 av = ld4(ap), bv = ld4(bp);
+    for (int rb = 0; rb < n_pad; rb += 8) {
+      const int nx = (rb + 8 < n_pad) ? rb + 8 : rb;
+      const f4 an = ld4(ap + nx), bn = ld4(bp + nx);
+      acc = mfma32(av[0], bv[0], acc);
+      acc = mfma32(av[1], bv[1], acc);
+      acc = mfma32(av[2], bv[2], acc);
+      acc = mfma32(av[3], bv[3], acc);
+      if (do_bias) bsum += (av[0] + av[1]) + (av[2] + av[3]);
+      av = an; bv = bn;
+    }
+    // Adam on the 32×32 sub-tile; lane holds rows (q&3)+8(q>>2)+4h, col lr.
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      f4 pt;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int q = qb * 4 + qq;
+        const int j = jrow0 + qq + 8 * qb + 4 * h;
+        const int64_t idx = pw + (int64_t)j * W + kcol;
+        float p = P[idx], mm = M[idx], vv = V[idx];
+        adam_update(p, mm, vv, acc[q], step_size, bc2s);
+        P[idx] = p; M[idx] = mm; V[idx] = vv;
+        pt[qq] = p;
+      }
+      st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
+    }
+    if (do_bias) {
+      bsum += __shfl_xor(bsum, 32, 64);
+      if (h == 0) {
+        const int64_t idx = pb + jrow0 + lr;
+        float p = P[idx], mm = M[idx], vv = V[idx];
+        adam_update(p, mm, vv, bsum, step_size, bc2s);
+        P[idx] = p; M[idx] = mm; V[idx] = vv;
+      }
+    }
+  } else {
+    // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0
+    const int u = t - L * TH - TF;
+    const float* pos = a.pos;
+    for (int f = 0; f < 16; ++f) {
+      const int j = u * 64 + wave * 16 + f;
+      const float* zp = SZ + (int64_t)j * n_pad;
+      float sw = 0.f, sb = 0.f;
+      for (int r4 = lane * 4; r4 < n_pad; r4 += 256) {
+        const f4 z = ld4(zp + r4), x = ld4(pos + r4);
+        sw += (z[0] * x[0] + z[1] * x[1]) + (z[2] * x[2] + z[3] * x[3]);
+        sb += (z[0] + z[1]) + (z[2] + z[3]);
+      }
+      sw = wave_sum(sw);
+      sb = wave_sum(sb);
+      if (lane == 0) {
+        float p = P[j], mm = M[j], vv = V[j];
+        adam_update(p, mm, vv, sw, step_size, bc2s);
+        P[j] = p; M[j] = mm; V[j] = vv;
+        p = P[W + j]; mm = M[W + j]; vv = V[W + j];
+        adam_update(p, mm, vv, sb, step_size, bc2s);
+        P[W + j] = p; M[W + j] = mm; V[W + j] = vv;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Prologue / epilogue helpers
+// ---------------------------------------------------------------------------
+
+// target_mean = y.mean(0); target_std = y.std(0).clamp(min=1e-3);
+// targets_norm = (y − mean)/std   (siren.py:85-87).  One thread per column.
+__global__ void k_normalize(KArgs a) {
+  const int fit = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.D) return;
+  const float* T = a.target + fit * a.t_stride;
+  float* TN = a.tnorm + fit * a.t_stride;
+  double s = 0.0;
+  for (int r = 0; r < a.N; ++r) s += (double)T[(int64_t)r * a.D + j];
+  const float mean = (float)(s / a.N);
+  double ss = 0.0;
+  for (int r = 0; r < a.N; ++r) {
+    const double d = (double)T[(int64_t)r * a.D + j] - (double)mean;
+    ss += d * d;
+  }
+  float sd = (float)sqrt(ss / (double)(a.N - 1));
+  sd = sd < 1e-3f ? 1e-3f : sd;
+  a.mean[fit * a.D + j] = mean;
+  a.stdv[fit * a.D + j] = sd;
+  for (int r = 0; r < a.n_pad; ++r) {
+    const int64_t o = (int64_t)r * a.D + j;
+    TN[o] = r < a.N ? (T[o] - mean) / sd : 0.f;
+  }
+}
+
+// params_t ← transposed copies of every hidden weight and of the final weight.
+__global__ void k_transpose_params(KArgs a) {
+  const int fit = blockIdx.y;
+  const int L = a.fit_layers[fit];
+  const int W = a.W, D = a.D;
+  const int64_t nh = (int64_t)L * W * W, total = nh + (int64_t)W * D;
+  const float* P = a.params + fit * a.p_stride;
+  float* PT = a.params_t + fit * a.pt_stride;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < nh) {
+      const int64_t i = e / ((int64_t)W * W), u = e % ((int64_t)W * W);
+      const int64_t k = u / W, j = u % W;  // PT_i[k][j] = W_i[j][k]
+      PT[e] = P[off_hidden_w(W, (int)i + 1) + j * W + k];
+    } else {
+      const int64_t u = e - nh;
+      const int64_t k = u / D, j = u % D;  // WfT[k][j] = Wf[j][k]
+      PT[e] = P[off_final_w(W, L) + j * W + k];
+    }
+  }
+}
+
+// Per-row metrics of pred_real = ŷ·std + mean against the raw target:
+// F.cosine_similarity(pred, y, dim=1) (eps 1e-8) and Σ_j (pred−y)².
+// (siren.py:109-111, 122-125).  One wave per row.
+__global__ void k_row_metrics(KArgs a, const float* ybuf, int64_t ystride,
+                              float* row_cos, float* row_sq, int64_t rstride) {
+  const int fit = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= a.n_pad) return;
+  const int D = a.D;
+  float* rc = row_cos + fit * rstride;
+  float* rs = row_sq + fit * rstride;
+  if (r >= a.N) {
+    if (lane == 0) { rc[r] = 0.f; rs[r] = 0.f; }
+    return;
+  }
+  const float* Y = ybuf + fit * ystride + (int64_t)r * D;
+  const float* T = a.target + fit * a.t_stride + (int64_t)r * D;
+  const float* mu = a.mean + fit * D;
+  const float* sd = a.stdv + fit * D;
+  float pp = 0.f, tt = 0.f, pt = 0.f, dd = 0.f;
+  for (int j = lane; j < D; j += 64) {
+    const float p = __fadd_rn(__fmul_rn(Y[j], sd[j]), mu[j]);
+    const float t = T[j];
+    const float d = p - t;
+    pp = fmaf(p, p, pp);
+    tt = fmaf(t, t, tt);
+    pt = fmaf(p, t, pt);
+    dd = fmaf(d, d, dd);
+  }
+  pp = wave_sum(pp); tt = wave_sum(tt); pt = wave_sum(pt); dd = wave_sum(dd);
+  if (lane == 0) {
+    const float n1 = fmaxf(sqrtf(pp), 1e-8f), n2 = fmaxf(sqrtf(tt), 1e-8f);
+    rc[r] = pt / (n1 * n2);
+    rs[r] = dd;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+
+bool width_ok(int W) { return W == 64 || W == 128 || W == 256 || W == 512; }
+bool dim_ok(int D) { return D == 64 || D == 128; }
+
+int validate(int W, int D, int N, int L_max, int epochs) {
+  if (!width_ok(W)) return NERFHIP_ERR_BAD_WIDTH;
+  if (!dim_ok(D)) return NERFHIP_ERR_BAD_HEAD_DIM;
+  if (L_max < 1 || L_max > NERFHIP_MAX_LAYERS) return NERFHIP_ERR_BAD_LAYERS;
+  if (N < 2 || epochs < 0) return NERFHIP_ERR_BAD_SHAPE;
+  return NERFHIP_OK;
+}
+
+void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
+  const int64_t n_pad = ((int64_t)N + kRowsPerBlock - 1) / kRowsPerBlock * kRowsPerBlock;
+  s->n_pad = n_pad;
+  s->params = n_params(W, D, L_max);
+  s->params_t = (int64_t)L_max * W * W + (int64_t)W * D;
+  s->scratch = 3 * (int64_t)(L_max + 1) * W * n_pad + (int64_t)D * n_pad;
+  s->target = n_pad * D;
+  s->stats = D;
+  s->loss_partial = (int64_t)epochs * (n_pad / 16);
+  s->rows = n_pad;
+}
+
+KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
+  KArgs a{};
+  a.W = g->W; a.D = g->D; a.N = g->N; a.n_pad = (int32_t)s.n_pad;
+  a.n_fits = g->n_fits; a.L_max = g->L_max; a.epochs = g->epochs;
+  a.p_stride = s.params; a.pt_stride = s.params_t; a.s_stride = s.scratch;
+  a.t_stride = s.target; a.lp_stride = s.loss_partial; a.y_stride = s.target;
+  a.fit_layers = g->fit_layers; a.fit_omega = g->fit_omega; a.pos = g->positions;
+  a.target = g->target; a.tnorm = g->target_norm; a.mean = g->mean; a.stdv = g->std;
+  a.params = g->params; a.params_t = g->params_t; a.m = g->adam_m; a.v = g->adam_v;
+  a.scratch = g->scratch; a.sched = g->sched; a.loss_partial = g->loss_partial;
+  // F.mse_loss backward: grad = (2/numel)·(ŷ−y), the 2/numel a python float
+  // rounded to fp32 (TORCH/_decomp/decompositions.py:393-397).
+  a.grad_scale = (float)(2.0 / ((double)g->N * (double)g->D));
+  return a;
+}
+
+int grid_for(int n_fits, int n_tiles) { return 8 * n_tiles * ((n_fits + 7) / 8); }
+
+template <int W, int D>
+int launch_rows(const KArgs& a, hipStream_t st) {
+  const int grid = grid_for(a.n_fits, a.n_pad / kRowsPerBlock);
+  hipLaunchKernelGGL((k_step_rows<W, D>), dim3(grid), dim3(kThreads), 0, st, a);
+  return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+
+template <int W, int D>
+int launch_params(const KArgs& a, hipStream_t st) {
+  constexpr int WT = W / 64;
+  const int n_tiles = a.L_max * WT * WT + (D / 64) * WT + WT;
+  const int grid = grid_for(a.n_fits, n_tiles);
+  hipLaunchKernelGGL((k_step_params<W, D>), dim3(grid), dim3(kThreads), 0, st, a);
+  return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+
+typedef int (*launch_fn)(const KArgs&, hipStream_t);
+
+template <int W>
+void pick_d(int D, launch_fn* rows, launch_fn* params) {
+  if (D == 64) { *rows = launch_rows<W, 64>; *params = launch_params<W, 64>; }
+  else { *rows = launch_rows<W, 128>; *params = launch_params<W, 128>; }
+}
+
+void pick(int W, int D, launch_fn* rows, launch_fn* params) {
+  switch (W) {
+    case 64: pick_d<64>(D, rows, params); break;
+    case 128: pick_d<128>(D, rows, params); break;
+    case 256: pick_d<256>(D, rows, params); break;
+    default: pick_d<512>(D, rows, params); break;
+  }
+}
+
+int row_metrics(const KArgs& a, const float* ybuf, int64_t ystride, float* rc, float* rs,
+                int64_t rstride, hipStream_t st) {
+  dim3 grid((unsigned)((a.n_pad + 3) / 4), (unsigned)a.n_fits);
+  hipLaunchKernelGGL(k_row_metrics, grid, dim3(256), 0, st, a, ybuf, ystride, rc, rs, rstride);
+  return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nerfhip_abi_version(void) { return NERFHIP_ABI_VERSION; }
+
+const char* nerfhip_status_string(int status) {
+  switch (status) {
+    case NERFHIP_OK: return "ok";
+    case NERFHIP_ERR_BAD_WIDTH: return "hidden_features must be one of 64, 128, 256, 512";
+    case NERFHIP_ERR_BAD_HEAD_DIM: return "d_head must be 64 or 128";
+    case NERFHIP_ERR_BAD_LAYERS: return "hidden_layers must be in [1, 4]";
+    case NERFHIP_ERR_BAD_SHAPE: return "bad shape (seq_len >= 2, n_fits >= 1, epochs >= 0)";
+    case NERFHIP_ERR_NULL: return "a required device pointer is NULL";
+    case NERFHIP_ERR_LAUNCH: return "kernel launch failed";
+    default: return "unknown nerfhip status";
+  }
+}
+
+int nerfhip_group_sizes(int32_t W, int32_t D, int32_t N, int32_t L_max, int32_t epochs,
+                        nerfhip_sizes* out) {
+  if (!out) return NERFHIP_ERR_NULL;
+  const int rc = validate(W, D, N, L_max, epochs);
+  if (rc != NERFHIP_OK) return rc;
+  fill_sizes(W, D, N, L_max, epochs, out);
+  return NERFHIP_OK;
+}
+
+static int check_group(const nerfhip_group* g, bool train) {
+  if (!g) return NERFHIP_ERR_NULL;
+  const int rc = validate(g->W, g->D, g->N, g->L_max, g->epochs);
+  if (rc != NERFHIP_OK) return rc;
+  if (g->n_fits < 1) return NERFHIP_ERR_BAD_SHAPE;
+  if (!g->fit_layers || !g->fit_omega || !g->positions || !g->params || !g->eval_y)
+    return NERFHIP_ERR_NULL;
+  if (train && (!g->target || !g->target_norm || !g->mean || !g->std || !g->params_t ||
+                !g->adam_m || !g->adam_v || !g->scratch || !g->sched || !g->loss_partial ||
+                !g->row_cos || !g->row_sq))
+    return NERFHIP_ERR_NULL;
+  if (train && g->log_every > 0 && g->epochs / g->log_every > 0 &&
+      (!g->probe_y || !g->probe_row_cos || !g->probe_row_sq))
+    return NERFHIP_ERR_NULL;
+  return NERFHIP_OK;
+}
+
+namespace {
+
+struct GroupRun {
+  const nerfhip_group* g;
+  hipStream_t st;
+  nerfhip_sizes s;
+  KArgs a;
+  launch_fn rows, params;
+  int n_probe;
+  int64_t probe_stride;
+};
+
+int select_device(int dev, int* cur) {
+  if (*cur == dev) return NERFHIP_OK;
+  if (hipSetDevice(dev) != hipSuccess) return NERFHIP_ERR_LAUNCH;
+  *cur = dev;
+  return NERFHIP_OK;
+}
+
+int prologue(GroupRun& r) {
+  const nerfhip_group* g = r.g;
+  // Adam state ← 0 (torch.optim.Adam lazy state init), normalise the target,
+  // transposed weight copies.
+  const size_t pbytes = (size_t)g->n_fits * r.s.params * sizeof(float);
+  if (hipMemsetAsync(g->adam_m, 0, pbytes, r.st) != hipSuccess) return NERFHIP_ERR_LAUNCH;
+  if (hipMemsetAsync(g->adam_v, 0, pbytes, r.st) != hipSuccess) return NERFHIP_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_normalize, dim3((g->D + 127) / 128, g->n_fits), dim3(128), 0, r.st, r.a);
+  hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st, r.a);
+  return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+
+int epoch_step(GroupRun& r, int e) {
+  KArgs& a = r.a;
+  a.epoch = e;
+  a.mode = 0;
+  a.y_out = nullptr;
+  if (r.n_probe > 0 && (e + 1) % r.g->log_every == 0) {
+    a.y_out = r.g->probe_y + (int64_t)((e + 1) / r.g->log_every - 1) * r.s.target;
+    a.y_stride = r.probe_stride;
+  }
+  int rc = r.rows(a, r.st);
+  if (rc == NERFHIP_OK) rc = r.params(a, r.st);
+  return rc;
+}
+
+int epilogue(GroupRun& r) {
+  // final evaluation (siren.py:119-125) and the probe metrics (siren.py:109-111)
+  KArgs& a = r.a;
+  const nerfhip_group* g = r.g;
+  a.mode = 1;
+  a.y_out = g->eval_y;
+  a.y_stride = r.s.target;
+  int rc = r.rows(a, r.st);
+  if (rc == NERFHIP_OK)
+    rc = row_metrics(a, g->eval_y, r.s.target, g->row_cos, g->row_sq, r.s.rows, r.st);
+  for (int k = 0; k < r.n_probe && rc == NERFHIP_OK; ++k)
+    rc = row_metrics(a, g->probe_y + k * r.s.target, r.probe_stride,
+                     g->probe_row_cos + k * r.s.rows, g->probe_row_sq + k * r.s.rows,
+                     (int64_t)r.n_probe * r.s.rows, r.st);
+  return rc;
+}
+
+GroupRun make_run(const nerfhip_group* g, void* stream) {
+  GroupRun r;
+  r.g = g;
+  r.st = (hipStream_t)stream;
+  fill_sizes(g->W, g->D, g->N, g->L_max, g->epochs, &r.s);
+  r.a = make_args(g, r.s);
+  pick(g->W, g->D, &r.rows, &r.params);
+  r.n_probe = g->log_every > 0 ? g->epochs / g->log_every : 0;
+  r.probe_stride = (int64_t)r.n_probe * r.s.target;
+  return r;
+}
+
+}  // namespace
+
+static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* streams,
+                    nerfhip_timing* timing) {
+  if (!groups || !streams || n_groups < 1) return NERFHIP_ERR_NULL;
+  for (int i = 0; i < n_groups; ++i) {
+    const int rc = check_group(&groups[i], true);
+    if (rc != NERFHIP_OK) return rc;
+  }
+  if (timing && (timing->group < 0 || timing->group >= n_groups)) return NERFHIP_ERR_BAD_SHAPE;
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess) return NERFHIP_ERR_LAUNCH;
+  int cur = prev;
+  GroupRun* runs = new GroupRun[n_groups];
+  int rc = NERFHIP_OK, max_epochs = 0;
+  for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
+    runs[i] = make_run(&groups[i], streams[i]);
+    if (groups[i].epochs > max_epochs) max_epochs = groups[i].epochs;
+    rc = select_device(groups[i].device, &cur);
+    if (rc == NERFHIP_OK) rc = prologue(runs[i]);
+  }
+  // timing: 3 events per epoch of the timed group (before rows, between, after params)
+  const int tg = timing ? timing->group : -1;
+  const int t_epochs = timing ? groups[tg].epochs : 0;
+  hipEvent_t* ev = nullptr;
+  if (timing && rc == NERFHIP_OK) {
+    rc = select_device(groups[tg].device, &cur);
+    ev = new hipEvent_t[3 * (size_t)t_epochs]();
+    for (int k = 0; k < 3 * t_epochs && rc == NERFHIP_OK; ++k)
+      if (hipEventCreate(&ev[k]) != hipSuccess) rc = NERFHIP_ERR_LAUNCH;
+  }
+  for (int e = 0; e < max_epochs && rc == NERFHIP_OK; ++e)
+    for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
+      if (e >= groups[i].epochs) continue;
+      rc = select_device(groups[i].device, &cur);
+      if (rc != NERFHIP_OK) break;
+      if (i == tg) {
+        GroupRun& r = runs[i];
+        KArgs& a = r.a;
+        a.epoch = e;
+        a.mode = 0;
+        a.y_out = nullptr;
+        if (r.n_probe > 0 && (e + 1) % r.g->log_every == 0) {
+          a.y_out = r.g->probe_y + (int64_t)((e + 1) / r.g->log_every - 1) * r.s.target;
+          a.y_stride = r.probe_stride;
+        }
+        (void)hipEventRecord(ev[3 * e], r.st);
+        rc = r.rows(a, r.st);
+        (void)hipEventRecord(ev[3 * e + 1], r.st);
+        if (rc == NERFHIP_OK) rc = r.params(a, r.st);
+        (void)hipEventRecord(ev[3 * e + 2], r.st);
+      } else {
+        rc = epoch_step(runs[i], e);
+      }
+    }
+  for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
+    rc = select_device(groups[i].device, &cur);
+    if (rc == NERFHIP_OK) rc = epilogue(runs[i]);
+  }
+  if (ev) {
+    if (rc == NERFHIP_OK && select_device(groups[tg].device, &cur) == NERFHIP_OK &&
+        hipStreamSynchronize(runs[tg].st) == hipSuccess) {
+      double rows_ms = 0.0, params_ms = 0.0;
+      for (int e = 0; e < t_epochs; ++e) {
+        float a = 0.f, b = 0.f;
+        (void)hipEventElapsedTime(&a, ev[3 * e], ev[3 * e + 1]);
+        (void)hipEventElapsedTime(&b, ev[3 * e + 1], ev[3 * e + 2]);
+        rows_ms += a;
+        params_ms += b;
+      }
+      timing->launches = t_epochs;
+      timing->rows_ms = rows_ms;
+      timing->params_ms = params_ms;
+    } else if (rc == NERFHIP_OK) {
+      rc = NERFHIP_ERR_LAUNCH;
+    }
+    for (int k = 0; k < 3 * t_epochs; ++k)
+      if (ev[k]) (void)hipEventDestroy(ev[k]);
+    delete[] ev;
+  }
+  delete[] runs;
+  if (cur != prev) (void)hipSetDevice(prev);
+  return rc;
+}
+
+int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const* streams) {
+  return fit_impl(groups, n_groups, streams, nullptr);
+}
+
+int nerfhip_siren_fit_timed(const nerfhip_group* groups, int32_t n_groups, void* const* streams,
+                            nerfhip_timing* timing) {
+  if (!timing) return NERFHIP_ERR_NULL;
+  return fit_impl(groups, n_groups, streams, timing);
+}
+
+int nerfhip_siren_forward(const nerfhip_group* g, void* stream) {
+  int rc = check_group(g, false);
+  if (rc != NERFHIP_OK) return rc;
+  GroupRun r = make_run(g, stream);
+  r.a.mode = 1;
+  r.a.y_out = g->eval_y;
+  r.a.y_stride = r.s.target;
+  rc = r.rows(r.a, r.st);
+  if (rc == NERFHIP_OK && g->target && g->mean && g->std && g->row_cos && g->row_sq)
+    rc = row_metrics(r.a, g->eval_y, r.s.target, g->row_cos, g->row_sq, r.s.rows, r.st);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,333 @@
+"""The fit farm: packs independent SIREN fits into device groups and runs them
+through the HIP engine (include/nerfhip.h) in one asynchronous call.
+
+Reference behaviour being replaced: `fit_kv_cache` calls `fit_siren` once per
+(layer, head, K|V, architecture) in a strictly sequential Python loop
+(nerf_attention/fit.py:303-319 of the reference = fit.py:54-76), each fit
+running its own 2000-iteration eager loop with a host sync per epoch
+(siren.py:98-105).  Here:
+
+* fits sharing (device, W, d_head, seq_len) form ONE group = one pair of
+  kernel launches per epoch for all of them (hidden_layers and omega_0 may
+  differ inside a group: medium/deep/hifreq/lofreq share W = 256);
+* every group gets its own HIP stream and the C side interleaves the groups'
+  launches epoch by epoch, so the groups run concurrently;
+* several devices can be driven from one process (`devices=[0, 1, ...]`),
+  fits assigned by longest-processing-time on the FLOP model of SURVEY §8d.
+  `bench.py` instead runs one process per GPU and passes `devices=[rank]`.
+
+There is deliberately no CPU path: a non-CUDA device raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _native
+from .schedule import adam_table
+from .types import SIRENConfig
+
+
+@dataclass
+class FitSpec:
+    """One fit: the raw KV slice [seq_len, d_head], its architecture and the
+    flat initial parameters in state_dict order (siren.py:89)."""
+    target: torch.Tensor
+    config: SIRENConfig
+    init: torch.Tensor
+
+
+@dataclass
+class FitOutput:
+    params: torch.Tensor          # flat fp32 [P] on the fit's device (state_dict order)
+    target_mean: torch.Tensor     # CPU [1, d]
+    target_std: torch.Tensor      # CPU [1, d]
+    losses: list                  # per-epoch normalised MSE (siren.py:105)
+    row_cos: np.ndarray           # [seq_len] final per-row cosine (siren.py:124)
+    row_mse: np.ndarray           # [seq_len] final per-row MSE (siren.py:125)
+    final_mse: float              # siren.py:123
+    probes: list = field(default_factory=list)  # (epoch, norm_mse, real_mse, cos)
+    train_time_seconds: float = 0.0
+    group_seconds: float = 0.0
+    device: int = 0
+
+
+def fit_flops(seq_len: int, d_head: int, cfg: SIRENConfig, epochs: int) -> float:
+    """Algorithmic FLOPs of one fit: GEMM multiply-adds × 2 of
+    forward + backward over `epochs`, plus the final evaluation forward."""
+    n, d, w, l = seq_len, d_head, cfg.hidden_features, cfg.hidden_layers
+    per_epoch = 6 * n * (l * w * w + w * d) + 4 * n * w
+    return float(epochs * per_epoch + 2 * n * (w + l * w * w + w * d))
+
+
+def fit_bytes(seq_len: int, d_head: int, cfg: SIRENConfig, epochs: int) -> float:
+    """Algorithmic HBM bytes of one fit: per epoch the target
+    once plus params/m/v read+written (24·P), activations assumed on-chip."""
+    p = cfg.num_parameters(d_head)
+    return float(epochs * (4 * seq_len * d_head + 24 * p) + 4 * seq_len * d_head)
+
+
+def lpt_partition(costs: list, n_bins: int) -> list:
+    """Longest-processing-time-first assignment of items to bins; returns the
+    bin index per item.  Deterministic (ties broken by item index)."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0.0] * n_bins
+    out = [0] * len(costs)
+    for i in order:
+        b = min(range(n_bins), key=lambda k: (load[k], k))
+        out[i] = b
+        load[b] += costs[i]
+    return out
+
+
+def resolve_device(device) -> torch.device:
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise _native.NerfhipError(
+            f"nerf-attention-amd trains on MI355X only (device={device!r}); there is no CPU "
+            "path. The reference CPU loop lives in oracle/ as a test checker.")
+    if not torch.cuda.is_available():
+        raise _native.NerfhipError("no HIP device visible (torch.cuda.is_available() is False)")
+    return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+class _Group:
+    """Device buffers + descriptor of one (device, W, d, seq_len) group."""
+
+    def __init__(self, members, specs, epochs, lr, log_every, device):
+        self.members = members
+        cfgs = [specs[i].config for i in members]
+        t0 = specs[members[0]].target
+        self.N, self.D = int(t0.shape[0]), int(t0.shape[1])
+        self.W = cfgs[0].hidden_features
+        self.L = [c.hidden_layers for c in cfgs]
+        self.L_max = max(self.L)
+        self.epochs = epochs
+        self.log_every = log_every if (log_every > 0 and epochs // log_every > 0) else 0
+        self.n_probe = epochs // self.log_every if self.log_every else 0
+        self.device = device
+        s = _native.group_sizes(self.W, self.D, self.N, self.L_max, epochs)
+        self.sizes = s
+        n, n_pad = len(members), int(s.n_pad)
+        self.n, self.n_pad = n, n_pad
+        dev = torch.device("cuda", device)
+        f32 = dict(dtype=torch.float32, device=dev)
+
+        # host-side packing (once per fit: the reference's H2D copies, siren.py:82-89)
+        pos = torch.zeros(n_pad, dtype=torch.float32)
+        pos[:self.N] = torch.linspace(0, 1, self.N)
+        tgt = torch.zeros(n, n_pad, self.D, dtype=torch.float32)
+        prm = torch.zeros(n, int(s.params), dtype=torch.float32)
+        for k, i in enumerate(members):
+            sp = specs[i]
+            if tuple(sp.target.shape) != (self.N, self.D):
+                raise ValueError("all fits of a group must share (seq_len, d_head)")
+            tgt[k, :self.N] = sp.target.detach().to("cpu", torch.float32)
+            p = sp.init.detach().to("cpu", torch.float32).reshape(-1)
+            if p.numel() != sp.config.num_parameters(self.D):
+                raise ValueError(f"init has {p.numel()} params, expected "
+                                 f"{sp.config.num_parameters(self.D)}")
+            prm[k, :p.numel()] = p
+        self.layers = torch.tensor(self.L, dtype=torch.int32, device=dev)
+        self.omega = torch.tensor([c.omega_0 for c in cfgs], **f32)
+        self.pos = pos.to(dev)
+        self.target = tgt.to(dev)
+        self.params_init = prm.to(dev)
+        self.params = self.params_init.clone()
+        self.sched = torch.from_numpy(adam_table(epochs, lr)).to(dev) if epochs > 0 \
+            else torch.zeros(1, 2, **f32)
+        self.target_norm = torch.empty(n, n_pad, self.D, **f32)
+        self.mean = torch.empty(n, self.D, **f32)
+        self.std = torch.empty(n, self.D, **f32)
+        self.params_t = torch.empty(n, int(s.params_t), **f32)
+        self.adam_m = torch.empty(n, int(s.params), **f32)
+        self.adam_v = torch.empty(n, int(s.params), **f32)
+        self.scratch = torch.empty(n, int(s.scratch), **f32)
+        self.loss_partial = torch.empty(n, max(int(s.loss_partial), 1), **f32)
+        self.eval_y = torch.empty(n, n_pad, self.D, **f32)
+        self.row_cos = torch.empty(n, n_pad, **f32)
+        self.row_sq = torch.empty(n, n_pad, **f32)
+        if self.n_probe:
+            self.probe_y = torch.empty(n, self.n_probe, n_pad, self.D, **f32)
+            self.probe_row_cos = torch.empty(n, self.n_probe, n_pad, **f32)
+            self.probe_row_sq = torch.empty(n, self.n_probe, n_pad, **f32)
+        else:
+            self.probe_y = self.probe_row_cos = self.probe_row_sq = None
+
+        ptr = lambda t: None if t is None else t.data_ptr()
+        self.desc = _native.NerfhipGroup(
+            W=self.W, D=self.D, N=self.N, n_fits=n, L_max=self.L_max, epochs=epochs,
+            log_every=self.log_every, device=device,
+            fit_layers=ptr(self.layers), fit_omega=ptr(self.omega), positions=ptr(self.pos),
+            target=ptr(self.target), target_norm=ptr(self.target_norm), mean=ptr(self.mean),
+            std=ptr(self.std), params=ptr(self.params), params_t=ptr(self.params_t),
+            adam_m=ptr(self.adam_m), adam_v=ptr(self.adam_v), scratch=ptr(self.scratch),
+            sched=ptr(self.sched), loss_partial=ptr(self.loss_partial),
+            probe_y=ptr(self.probe_y), eval_y=ptr(self.eval_y), row_cos=ptr(self.row_cos),
+            row_sq=ptr(self.row_sq), probe_row_cos=ptr(self.probe_row_cos),
+            probe_row_sq=ptr(self.probe_row_sq))
+        with torch.cuda.device(dev):
+            self.stream = torch.cuda.Stream(device=dev)
+            self.stream.wait_stream(torch.cuda.current_stream(dev))  # H2D copies above
+            self.ev_start = torch.cuda.Event(enable_timing=True)
+            self.ev_end = torch.cuda.Event(enable_timing=True)
+
+    def outputs(self, specs, group_seconds):
+        N, D, n = self.N, self.D, self.n
+        numel = float(N * D)
+        E = self.epochs
+        if E > 0:
+            lp = self.loss_partial[:, :E * (self.n_pad // 16)].view(n, E, self.n_pad // 16)
+            losses = (lp.double().sum(-1) / numel).float().cpu().numpy()
+        else:
+            losses = np.zeros((n, 0), np.float32)
+        row_cos = self.row_cos[:, :N].cpu().numpy()
+        row_sq = self.row_sq[:, :N].cpu()
+        final_mse = (row_sq.double().sum(-1) / numel).float().numpy()
+        row_mse = (row_sq / D).numpy()
+        mean = self.mean.cpu()
+        std = self.std.cpu()
+        if self.n_probe:
+            p_cos = torch.from_numpy(self.probe_row_cos[:, :, :N].cpu().numpy())
+            p_sq = self.probe_row_sq[:, :, :N].cpu().double().sum(-1) / numel
+            p_cos_mean = p_cos.mean(-1)
+        flops = [fit_flops(N, D, specs[i].config, E) for i in self.members]
+        tot = sum(flops) or 1.0
+        outs = []
+        for k, i in enumerate(self.members):
+            P = specs[i].config.num_parameters(D)
+            probes = []
+            for q in range(self.n_probe):
+                ep = (q + 1) * self.log_every
+                probes.append((ep, float(losses[k, ep - 1]), float(np.float32(p_sq[k, q])),
+                               float(p_cos_mean[k, q])))
+            outs.append(FitOutput(
+                params=self.params[k, :P], target_mean=mean[k].view(1, D).clone(),
+                target_std=std[k].view(1, D).clone(),
+                losses=[float(x) for x in losses[k]], row_cos=row_cos[k].copy(),
+                row_mse=row_mse[k].copy(), final_mse=float(final_mse[k]), probes=probes,
+                train_time_seconds=group_seconds * flops[k] / tot,
+                group_seconds=group_seconds, device=self.device))
+        return outs
+
+
+def plan_groups(specs: list, devices: list) -> list:
+    """[(device, [spec indices])] — LPT over devices, then (W, d, seq_len)."""
+    costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
+             for s in specs]
+    dev_of = lpt_partition(costs, len(devices)) if len(devices) > 1 else [0] * len(specs)
+    keys = {}
+    for i, s in enumerate(specs):
+        k = (devices[dev_of[i]], s.config.hidden_features, int(s.target.shape[1]),
+             int(s.target.shape[0]))
+        keys.setdefault(k, []).append(i)
+    # heaviest groups first: they are enqueued (and start) first
+    return sorted(((k[0], m) for k, m in keys.items()),
+                  key=lambda dm: -sum(costs[i] for i in dm[1]))
+
+
+class FitJob:
+    """A set of fits with every input already resident on its device.
+
+    launch() enqueues the whole training (all groups, all epochs) and returns;
+    wait() blocks; outputs() reads the results.  reset() restores the initial
+    parameters so the same job can be launched again (bench.py's steps)."""
+
+    def __init__(self, specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
+                 devices=None):
+        _native.load()
+        if devices is None:
+            devices = [resolve_device("cuda").index]
+        self.devices = [resolve_device(torch.device("cuda", d)).index for d in devices]
+        self.specs = specs
+        self.epochs = epochs
+        self.plan = plan_groups(specs, self.devices)
+        self.groups = [_Group(m, specs, epochs, lr, log_every, d) for d, m in self.plan]
+        G = len(self.groups)
+        self._descs = (_native.NerfhipGroup * G)(*[g.desc for g in self.groups])
+        self._streams = (ctypes.c_void_p * G)(*[g.stream.cuda_stream for g in self.groups])
+        self.fresh = True
+        self.timing = None
+
+    def reset(self) -> None:
+        for g in self.groups:
+            with torch.cuda.stream(g.stream):
+                g.params.copy_(g.params_init, non_blocking=True)
+        self.fresh = True
+
+    def launch(self, time_group: int | None = None) -> None:
+        """Enqueue every group.  time_group: index into self.groups whose two
+        step kernels get hipEvent timing (synchronises that group)."""
+        if not self.fresh:
+            self.reset()
+        self.fresh = False
+        G = len(self.groups)
+        for g in self.groups:
+            g.ev_start.record(g.stream)
+        if time_group is None:
+            _native.check(_native.load().nerfhip_siren_fit(self._descs, G, self._streams))
+            self.timing = None
+        else:
+            t = _native.NerfhipTiming(group=time_group)
+            _native.check(_native.load().nerfhip_siren_fit_timed(self._descs, G, self._streams,
+                                                                 ctypes.byref(t)))
+            self.timing = t
+        for g in self.groups:
+            g.ev_end.record(g.stream)
+
+    def wait(self) -> None:
+        for g in self.groups:
+            g.ev_end.synchronize()
+
+    def group_seconds(self) -> list:
+        return [g.ev_start.elapsed_time(g.ev_end) / 1e3 for g in self.groups]
+
+    def outputs(self) -> list:
+        outs = [None] * len(self.specs)
+        for g, secs in zip(self.groups, self.group_seconds()):
+            for i, o in zip(g.members, g.outputs(self.specs, secs)):
+                outs[i] = o
+        return outs
+
+
+def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
+             devices=None) -> list:
+    """Train every FitSpec for `epochs` Adam steps; returns FitOutput per spec
+    (same order).  Blocks until the device work is done."""
+    if not specs:
+        return []
+    job = FitJob(specs, epochs, lr, log_every, devices)
+    job.launch()
+    job.wait()
+    return job.outputs()
+
+
+def forward(params: torch.Tensor, config: SIRENConfig, d_head: int,
+            positions: torch.Tensor) -> torch.Tensor:
+    """SIREN forward on the HIP engine (inference; siren.py:60-61).
+    params: flat fp32 state_dict-order vector on a CUDA device;
+    positions: [n] or [n, 1] on the same device.  Returns [n, d_head]."""
+    dev = params.device
+    n = int(positions.numel())
+    s = _native.group_sizes(config.hidden_features, d_head, n, config.hidden_layers, 0)
+    n_pad = int(s.n_pad)
+    pos = torch.zeros(n_pad, dtype=torch.float32, device=dev)
+    pos[:n] = positions.reshape(-1).to(torch.float32)
+    prm = params.detach().to(torch.float32).contiguous()
+    layers = torch.tensor([config.hidden_layers], dtype=torch.int32, device=dev)
+    omega = torch.tensor([config.omega_0], dtype=torch.float32, device=dev)
+    y = torch.empty(n_pad, d_head, dtype=torch.float32, device=dev)
+    g = _native.NerfhipGroup(W=config.hidden_features, D=d_head, N=n, n_fits=1,
+                             L_max=config.hidden_layers, epochs=0, log_every=0,
+                             device=dev.index, fit_layers=layers.data_ptr(),
+                             fit_omega=omega.data_ptr(), positions=pos.data_ptr(),
+                             params=prm.data_ptr(), eval_y=y.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+    _native.check(_native.load().nerfhip_siren_forward(ctypes.byref(g), stream.cuda_stream))
+    return y[:n]

@@ -1,0 +1,238 @@
+"""Sweep driver: fit SIRENs to an extracted KV cache — `python -m nerf_attention.fit`.
+
+Drop-in for the reference driver (nerf_attention/fit.py:20-196): same
+signature, CLI flags, selection rules, record order, stdout lines,
+`fit_results.json` schema (19 keys, indent=2) and `{name}_model.pt`
+checkpoints for the medium architecture.
+
+What changes is HOW the fits run.  The reference trains them one after
+another (fit.py:54-76).  Here every model is first initialised on the host in
+the reference's loop order — init is the only consumer of the torch RNG, so
+each fit gets exactly the parameters the sequential reference would give it —
+and then ALL fits are trained together on the HIP engine (grouped by width,
+one stream per group, optionally over several GPUs).  The per-fit progress
+lines are printed afterwards, in the reference order.
+
+`train_time_seconds` is each fit's share of its group's device time
+(group time × fit FLOPs / group FLOPs): fits of a group train concurrently,
+so the reference's per-fit wall clock has no direct equivalent.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from . import engine
+from .siren import SIREN, _finish, probe_line
+from .types import CONFIGS_FULL, CONFIGS_QUICK, FitResult, KVMetadata, SIRENConfig
+
+
+def select_fits(metadata: KVMetadata, quick: bool):
+    """(layers, heads_per_layer, configs) — reference fit.py:39-48."""
+    nl = metadata.num_layers
+    if quick:
+        layers = [0, nl // 2, nl - 1]
+        heads, configs = 1, CONFIGS_QUICK
+    else:
+        layers = [0, nl // 4, nl // 2, 3 * nl // 4, nl - 1]
+        heads, configs = min(metadata.num_kv_heads, 4), CONFIGS_FULL
+    layers = sorted(set(l for l in layers if l < nl))
+    return layers, heads, configs
+
+
+def sweep_plan(layers, heads, configs, load_layer):
+    """Fits in the reference record order layer → head → (key, value) → config
+    (fit.py:54-65).  load_layer(l) returns {'keys','values'} or None (skip)."""
+    plan, skipped = [], []
+    for layer in layers:
+        data = load_layer(layer)
+        if data is None:
+            skipped.append(layer)
+            continue
+        for head in range(heads):
+            for kv_type, tensor in (('key', data['keys'][head]), ('value', data['values'][head])):
+                for cfg in configs:
+                    plan.append((f"L{layer}_H{head}_{kv_type}_{cfg.name}", layer, head, kv_type,
+                                 cfg, tensor))
+    return plan, skipped
+
+
+def train_plan(plan, epochs: int, devices, log_every: int):
+    """Initialise every model in plan order (the reference's RNG order), then
+    train them all on the engine.  Returns [(FitResult, probes)]."""
+    models, specs = [], []
+    for _name, _l, _h, _kv, cfg, tensor in plan:
+        m = SIREN(cfg, out_features=int(tensor.shape[1]))
+        models.append(m)
+        specs.append(engine.FitSpec(target=tensor, config=cfg, init=m.flat_parameters()))
+    outs = engine.run_fits(specs, epochs, log_every=log_every, devices=devices)
+    results = []
+    for (name, _l, _h, _kv, cfg, tensor), m, o in zip(plan, models, outs):
+        m = m.to(torch.device('cuda', o.device))
+        m.load_flat_parameters(o.params)
+        m.eval()
+        results.append((_finish(m, cfg, o, int(tensor.shape[0]), int(tensor.shape[1])),
+                        o.probes))
+    return results
+
+
+def fit_kv_cache(
+    kv_dir: Path,
+    output_dir: Path,
+    epochs: int = 5000,
+    device: str = 'cuda',
+    quick: bool = False,
+    *,
+    gpus: int | None = None,
+) -> list[dict]:
+    """Fit SIRENs to an extracted KV cache and record metrics (fit.py:20-92).
+    `gpus` (extension): farm the fits over this many local GPUs."""
+    kv_dir, output_dir = Path(kv_dir), Path(output_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    with open(kv_dir / 'metadata.json') as f:
+        metadata = KVMetadata.from_dict(json.load(f))
+
+    print(f"KV Cache: {metadata.num_layers} layers x {metadata.num_kv_heads} heads")
+    print(f"Per tensor: ({metadata.seq_len}, {metadata.head_dim}) = "
+          f"{metadata.seq_len * metadata.head_dim * 2 / 1024:.1f} KB (float16 baseline)")
+    print(f"Device: {device}, Epochs: {epochs}")
+
+    dev = engine.resolve_device(device)
+    devices = [dev.index] if not gpus or gpus <= 1 else list(range(gpus))
+    layers, heads, configs = select_fits(metadata, quick)
+    total = len(layers) * heads * 2 * len(configs)
+
+    def load_layer(layer):
+        p = kv_dir / f'layer_{layer:02d}.pt'
+        if not p.exists():
+            return None
+        return torch.load(p, map_location='cpu', weights_only=True)
+
+    plan, skipped = sweep_plan(layers, heads, configs, load_layer)
+    results = train_plan(plan, epochs, devices, log_every=max(epochs // 5, 100))
+
+    all_results: list[dict] = []
+    count = 0
+    for layer in layers:
+        if layer in skipped:
+            print(f"  Skipping layer {layer} (not found)")
+            continue
+        for (name, l, head, kv_type, cfg, _t), (res, probes) in zip(plan, results):
+            if l != layer:
+                continue
+            count += 1
+            print(f"\n[{count}/{total}] {name}")
+            for ep, nm, rm, cs in probes:
+                print(probe_line(ep, epochs, nm, rm, cs))
+            record = _result_to_record(name, layer, head, kv_type, res)
+            all_results.append(record)
+            if cfg.name == 'medium':
+                _save_model(output_dir, name, res, record)
+            print(f"  -> CosSim: {res.final_cosine_mean:.4f} | "
+                  f"Compress: {res.compression_ratio:.1f}x | "
+                  f"Time: {res.train_time_seconds:.1f}s")
+
+    with open(output_dir / 'fit_results.json', 'w') as f:
+        json.dump(all_results, f, indent=2)
+    _print_summary(all_results, layers)
+    return all_results
+
+
+RECORD_KEYS = ('name', 'layer', 'head', 'kv_type', 'config_name', 'hidden_features',
+               'hidden_layers', 'omega_0', 'final_mse', 'final_cosine_mean',
+               'final_cosine_min', 'final_cosine_std', 'compression_ratio', 'raw_size_bytes',
+               'siren_size_bytes', 'train_time_seconds', 'num_parameters', 'seq_len', 'd_head')
+
+
+def _result_to_record(name: str, layer: int, head: int, kv_type: str,
+                      result: FitResult) -> dict:
+    """The 19-key JSON record of fit.py:95-118, in that key order."""
+    c = result.config
+    values = (name, layer, head, kv_type, c.name, c.hidden_features, c.hidden_layers, c.omega_0,
+              result.final_mse, result.final_cosine_mean, result.final_cosine_min,
+              result.final_cosine_std, result.compression_ratio, result.raw_size_bytes,
+              result.siren_size_bytes, result.train_time_seconds, result.num_parameters,
+              result.seq_len, result.d_head)
+    return dict(zip(RECORD_KEYS, values))
+
+
+def _save_model(output_dir: Path, name: str, result: FitResult, record: dict) -> None:
+    """{name}_model.pt as fit.py:121-137 writes it (read by evaluate.py:34-45)."""
+    c = result.config
+    ckpt = {
+        'model_state': result.model.state_dict(),
+        'config': {'hidden_features': c.hidden_features, 'hidden_layers': c.hidden_layers,
+                   'omega_0': c.omega_0, 'name': c.name, 'out_features': result.d_head},
+        'target_mean': result.target_mean,
+        'target_std': result.target_std,
+        'metrics': record,
+    }
+    torch.save(ckpt, output_dir / f'{name}_model.pt')
+
+
+def _print_summary(all_results: list[dict], layers_to_fit: list[int]) -> None:
+    """Results table and per-architecture / K-V / layer means (fit.py:140-180)."""
+    bar = '=' * 80
+    print(f"\n{bar}\nRESULTS SUMMARY\n{bar}")
+    print(f"{'Name':<35} {'CosSim':>8} {'MSE':>10} {'Compress':>10} {'Time':>8}")
+    print(f"{'-' * 35} {'-' * 8} {'-' * 10} {'-' * 10} {'-' * 8}")
+    for r in sorted(all_results, key=lambda x: x['final_cosine_mean'], reverse=True):
+        print(f"{r['name']:<35} {r['final_cosine_mean']:>8.4f} "
+              f"{r['final_mse']:>10.6f} {r['compression_ratio']:>9.1f}x "
+              f"{r['train_time_seconds']:>7.1f}s")
+    print(f"\n{bar}\nKEY FINDINGS\n{bar}")
+    for cn in sorted({r['config_name'] for r in all_results}):
+        cr = [r for r in all_results if r['config_name'] == cn]
+        print(f"  {cn:<10}: avg CosSim={np.mean([r['final_cosine_mean'] for r in cr]):.4f}, "
+              f"avg Compression={np.mean([r['compression_ratio'] for r in cr]):.1f}x")
+    keys = [r['final_cosine_mean'] for r in all_results if r['kv_type'] == 'key']
+    vals = [r['final_cosine_mean'] for r in all_results if r['kv_type'] == 'value']
+    if keys and vals:
+        k_avg, v_avg = np.mean(keys), np.mean(vals)
+        print(f"\n  Keys avg CosSim:   {k_avg:.4f}")
+        print(f"  Values avg CosSim: {v_avg:.4f}")
+        diff = v_avg - k_avg
+        if diff > 0.01:
+            print("  -> Values compress better (smoother signal)")
+        elif diff < -0.01:
+            print("  -> Keys compress better (stronger positional structure)")
+        else:
+            print("  -> Similar compressibility")
+    for layer in layers_to_fit:
+        lr = [r['final_cosine_mean'] for r in all_results
+              if r['layer'] == layer and r['config_name'] == 'medium']
+        if lr:
+            print(f"  Layer {layer:2d} (medium): avg CosSim={np.mean(lr):.4f}")
+
+
+def main() -> None:
+    parser = argparse.ArgumentParser(description='Fit SIRENs to KV cache')
+    parser.add_argument('--kv_dir', type=str, default='results/kv_cache')
+    parser.add_argument('--output_dir', type=str, default='results/fits')
+    parser.add_argument('--epochs', type=int, default=5000)
+    parser.add_argument('--device', type=str, default='cuda')
+    parser.add_argument('--quick', action='store_true')
+    parser.add_argument('--gpus', type=int, default=1,
+                        help='farm the fits over this many local GPUs (extension)')
+    parser.add_argument('--seed', type=int, default=None,
+                        help='torch.manual_seed before the sweep (extension; the reference '
+                             'is unseeded)')
+    args = parser.parse_args()
+    if args.seed is not None:
+        torch.manual_seed(args.seed)
+    # The reference falls back to CPU when CUDA is missing (fit.py:192-194);
+    # this engine has no CPU path, so resolve_device raises instead.
+    t0 = time.time()
+    fit_kv_cache(Path(args.kv_dir), Path(args.output_dir), args.epochs, args.device,
+                 args.quick, gpus=args.gpus)
+    print(f"\n[nerf-attention-amd] sweep wall clock {time.time() - t0:.2f}s")
+
+
+if __name__ == '__main__':
+    main()

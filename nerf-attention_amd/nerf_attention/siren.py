@@ -1,0 +1,161 @@
+"""SIREN model and `fit_siren` — the MI355X drop-in for the reference hot path.
+
+Reference: nerf_attention/siren.py.  `SineLayer` / `SIREN` (siren.py:17-67)
+keep the reference's module tree, state_dict keys
+(`network.{0..L}.linear.{weight,bias}`, `network.{L+1}.{weight,bias}`) and —
+crucially for seeded parity — its exact CPU-RNG consumption order:
+`nn.Linear.__init__` (kaiming_uniform_ weight, uniform_ bias), then the
+SIREN re-draw of weight then bias.  Initialisation is the only RNG consumer
+of a fit, so a fit started from the same torch seed starts from the same
+parameters as the reference.
+
+`fit_siren` (siren.py:70-149) keeps the reference signature and returns the
+same `FitResult`, but the 2000-epoch loop runs on the HIP engine: two fused
+kernels per epoch, no per-epoch host sync, metrics computed on the device.
+There is no CPU fallback: device='cpu' raises.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import engine
+from .types import FitResult, SIRENConfig
+
+
+class SineLayer(nn.Module):
+    """y = sin(ω0 · (x Wᵀ + b)) — reference siren.py:17-34."""
+
+    def __init__(self, in_features: int, out_features: int,
+                 omega_0: float = 30.0, is_first: bool = False):
+        super().__init__()
+        self.omega_0 = omega_0
+        # nn.Linear's own reset_parameters consumes the RNG first (as in the reference)
+        self.linear = nn.Linear(in_features, out_features)
+        if is_first:
+            bound = 1.0 / in_features
+        else:
+            bound = math.sqrt(6.0 / in_features) / omega_0
+        with torch.no_grad():
+            self.linear.weight.uniform_(-bound, bound)
+            self.linear.bias.uniform_(-bound, bound)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return torch.sin(self.omega_0 * self.linear(x))
+
+
+class SIREN(nn.Module):
+    """SineLayer(1, W, first) → L × SineLayer(W, W) → Linear(W, d) — siren.py:37-67."""
+
+    def __init__(self, config: SIRENConfig, out_features: int):
+        super().__init__()
+        self.siren_config = config
+        w, om = config.hidden_features, config.omega_0
+        stack: list[nn.Module] = [SineLayer(1, w, omega_0=om, is_first=True)]
+        stack += [SineLayer(w, w, omega_0=om) for _ in range(config.hidden_layers)]
+        head = nn.Linear(w, out_features)
+        bound = math.sqrt(6.0 / w) / om
+        with torch.no_grad():
+            head.weight.uniform_(-bound, bound)
+            head.bias.uniform_(-bound, bound)
+        stack.append(head)
+        self.network = nn.Sequential(*stack)
+        self.out_features = out_features
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        # Inference on a CUDA device goes through the HIP forward kernel; with
+        # autograd recording (training through this module) or on the CPU the
+        # module is plain torch, as a CPU nn.Module must be.
+        if x.is_cuda and not (torch.is_grad_enabled() and
+                              any(p.requires_grad for p in self.parameters())):
+            return engine.forward(self.flat_parameters(), self.siren_config,
+                                  self.out_features, x).to(x.dtype)
+        return self.network(x)
+
+    def flat_parameters(self) -> torch.Tensor:
+        """All parameters concatenated in state_dict order (the engine's layout)."""
+        return torch.cat([p.detach().reshape(-1) for p in self.state_dict().values()])
+
+    @torch.no_grad()
+    def load_flat_parameters(self, flat: torch.Tensor) -> None:
+        off = 0
+        for p in self.state_dict().values():
+            n = p.numel()
+            p.copy_(flat[off:off + n].view_as(p))
+            off += n
+
+    def count_parameters(self) -> int:
+        return sum(p.numel() for p in self.parameters() if p.requires_grad)
+
+    def size_bytes(self) -> int:
+        return self.count_parameters() * 4
+
+
+def _finish(model: SIREN, config: SIRENConfig, out: engine.FitOutput, seq_len: int,
+            d_head: int) -> FitResult:
+    """FitResult exactly as siren.py:127-149 assembles it."""
+    cos = torch.from_numpy(out.row_cos)
+    raw_size = seq_len * d_head * 2
+    siren_size = model.size_bytes()
+    return FitResult(
+        model=model,
+        config=config,
+        target_mean=out.target_mean,
+        target_std=out.target_std,
+        losses=out.losses,
+        final_mse=out.final_mse,
+        final_cosine_mean=cos.mean().item(),
+        final_cosine_min=cos.min().item(),
+        final_cosine_std=cos.std().item(),
+        per_pos_mse=out.row_mse,
+        cosine_sims=out.row_cos,
+        compression_ratio=raw_size / siren_size,
+        raw_size_bytes=raw_size,
+        siren_size_bytes=siren_size,
+        train_time_seconds=out.train_time_seconds,
+        seq_len=seq_len,
+        d_head=d_head,
+        num_parameters=model.count_parameters(),
+    )
+
+
+def probe_line(epoch: int, epochs: int, norm_mse: float, real_mse: float, cos: float) -> str:
+    """The verbose progress line of siren.py:112-115."""
+    return (f"  Epoch {epoch}/{epochs} | "
+            f"NormMSE: {norm_mse:.6f} | "
+            f"RealMSE: {real_mse:.6f} | "
+            f"CosSim: {cos:.4f}")
+
+
+def fit_siren(
+    kv_tensor: torch.Tensor,
+    config: SIRENConfig,
+    epochs: int = 5000,
+    lr: float = 1e-4,
+    device: str = 'cuda',
+    log_every: int = 500,
+    verbose: bool = True,
+) -> FitResult:
+    """Fit a SIREN to one (seq_len, d_head) KV tensor on the MI355X engine.
+
+    Same contract as the reference (siren.py:70-149): the input is not
+    mutated, the torch CPU RNG is consumed exactly once (model init), the
+    result owns its model (on `device`) and CPU copies of mean/std/metrics.
+    """
+    seq_len, d_head = kv_tensor.shape
+    dev = engine.resolve_device(device)
+    model = SIREN(config, out_features=d_head)
+    spec = engine.FitSpec(target=kv_tensor, config=config, init=model.flat_parameters())
+    out = engine.run_fits([spec], epochs, lr=lr, log_every=log_every if verbose else 0,
+                          devices=[dev.index])[0]
+    model = model.to(dev)
+    model.load_flat_parameters(out.params)
+    model.eval()  # siren.py:119
+    if verbose:
+        for ep, nm, rm, cs in out.probes:
+            print(probe_line(ep, epochs, nm, rm, cs))
+    return _finish(model, config, out, seq_len, d_head)
