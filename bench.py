@@ -102,14 +102,13 @@ def main() -> None:
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
 
-    from nerf_attention import engine
+    from nerf_attention import engine, farm
     from nerf_attention.workloads import sweep_280
 
     plan, specs = sweep_280(args.seq_len, seed=0)
     n_total = len(specs)
     costs = [engine.fit_flops(args.seq_len, 128, s.config, args.epochs) for s in specs]
-    owner = engine.lpt_partition(costs, world) if world > 1 else [0] * n_total
-    mine = [i for i in range(n_total) if owner[i] == rank]
+    mine = farm.rank_share(costs, world, rank)
     job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[local])
 
     # dominant group on this rank = the one with the most FLOPs
@@ -122,11 +121,7 @@ def main() -> None:
         job.launch()
         job.wait()
 
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
+    barrier = farm.barrier
     barrier()
     t0 = time.perf_counter()
     rows_ms = params_ms = 0.0
@@ -140,20 +135,12 @@ def main() -> None:
             launches += job.timing.launches
     barrier()
     elapsed = time.perf_counter() - t0
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    t_max = float(t_max.item())
+    t_max = farm.max_over_ranks(elapsed)
 
     # per-fit results for the parity summary (host-side gather; not timed)
     outs = job.outputs()
     my_cos = {mine[k]: float(torch.from_numpy(o.row_cos).mean()) for k, o in enumerate(outs)}
-    if world > 1:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, my_cos)
-        all_cos = {k: v for d in gathered for k, v in d.items()}
-    else:
-        all_cos = my_cos
+    all_cos = farm.gather_records(my_cos)
 
     if rank == 0:
         value = n_total * args.steps / t_max

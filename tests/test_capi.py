@@ -1,0 +1,80 @@
+"""The C-ABI library: builds for gfx950, loads, exports every symbol the
+header declares, and validates its arguments — no GPU compute here."""
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from nerf_attention import _build, _native
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "nerfhip.h"
+
+
+@pytest.fixture(scope="module")
+def lib():
+    _build.build(verbose=False)
+    return _native.load()
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(nerfhip_\w+)\s*\(", text,
+                                 flags=re.M)))
+
+
+def test_header_symbols_exported(lib):
+    names = declared_functions()
+    assert names == sorted(_native.SIGNATURES), names
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_build.LIB)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (nerfhip_\w+)", out))
+    assert set(names) <= exported
+    for n in names:
+        assert getattr(lib, n)
+
+
+def test_code_object_is_gfx950(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading",
+                          str(_build.LIB)], capture_output=True, text=True, cwd="/tmp")
+    assert "gfx950" in (out.stdout + out.stderr)
+
+
+def test_abi_and_status(lib):
+    assert lib.nerfhip_abi_version() == _native.ABI_VERSION
+    assert lib.nerfhip_status_string(0) == b"ok"
+    assert b"hidden_features" in lib.nerfhip_status_string(-1)
+
+
+@pytest.mark.parametrize("W,D,N,L,E", [(256, 128, 2048, 3, 2000), (64, 64, 130, 1, 5)])
+def test_group_sizes(lib, W, D, N, L, E):
+    s = _native.group_sizes(W, D, N, L, E)
+    n_pad = (N + 63) // 64 * 64
+    assert s.n_pad == n_pad
+    assert s.params == 2 * W + L * (W * W + W) + W * D + D
+    assert s.params_t == L * W * W + W * D
+    assert s.scratch == 3 * (L + 1) * W * n_pad + D * n_pad
+    assert s.target == n_pad * D and s.rows == n_pad
+    assert s.loss_partial == E * n_pad // 16
+
+
+@pytest.mark.parametrize("args,code", [((96, 128, 64, 1, 1), -1), ((64, 96, 64, 1, 1), -2),
+                                       ((64, 128, 64, 0, 1), -3), ((64, 128, 64, 5, 1), -3),
+                                       ((64, 128, 1, 1, 1), -4), ((64, 128, 64, 1, -1), -4)])
+def test_group_sizes_rejects(lib, args, code):
+    s = _native.NerfhipSizes()
+    assert lib.nerfhip_group_sizes(*args, ctypes.byref(s)) == code
+
+
+def test_fit_rejects_before_touching_device(lib):
+    g = _native.NerfhipGroup(W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=10)
+    streams = (ctypes.c_void_p * 1)(None)
+    assert lib.nerfhip_siren_fit(ctypes.byref(g), 1, streams) == -5       # NULL buffers
+    g.W = 100
+    assert lib.nerfhip_siren_fit(ctypes.byref(g), 1, streams) == -1
+    assert lib.nerfhip_siren_fit(None, 1, streams) == -5
+    t = _native.NerfhipTiming(group=3)
+    assert lib.nerfhip_siren_fit_timed(ctypes.byref(g), 1, streams, None) == -5
+    assert lib.nerfhip_siren_forward(None, None) == -5

@@ -1,0 +1,182 @@
+"""Host-side logic of the product package (no GPU): model init and its RNG
+order, the synthetic KV generator, the optimiser schedule, sweep selection and
+ordering, record / checkpoint schema, LPT sharding."""
+
+import hashlib
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from nerf_attention import CONFIGS_FULL, SIREN, SIRENConfig, types
+from nerf_attention import engine, schedule
+from nerf_attention.fit import (RECORD_KEYS, _result_to_record, _save_model, select_fits,
+                                sweep_plan)
+from nerf_attention.siren import _finish
+from nerf_attention.synthetic import kv_layer, kv_slice
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_init_matches_reference(golden_dir):
+    g = json.loads((golden_dir / "init.json").read_text())
+    arrays = np.load(golden_dir / "init_tiny_small.npz")
+    for name, rec in g.items():
+        cfg = SIRENConfig(rec["hidden_features"], rec["hidden_layers"], rec["omega_0"], name)
+        torch.manual_seed(0)
+        m = SIREN(cfg, 128)
+        flat = m.flat_parameters().numpy()
+        assert list(m.state_dict().keys()) == rec["keys"]
+        assert flat.size == rec["num_parameters"] == cfg.num_parameters(128)
+        assert m.count_parameters() == rec["num_parameters"]
+        assert sha(flat) == rec["sha256"], name
+        if name in arrays:
+            assert np.array_equal(flat, arrays[name])
+
+
+def test_sweep_init_order(golden_dir):
+    """Pre-generating the 280 inits in loop order == the reference's sequential run."""
+    ref = json.loads((golden_dir / "sweep_init_order.json").read_text())
+    cfg = {c.name: c for c in CONFIGS_FULL}
+    torch.manual_seed(0)
+    for name, h in ref:
+        m = SIREN(cfg[name.split("_")[-1]], 128)
+        assert sha(m.flat_parameters().numpy()) == h, name
+
+
+def test_synthetic_quickstart_bit_exact(golden_dir):
+    g = json.loads((golden_dir / "synthetic.json").read_text())["q512"]
+    for l in range(4):
+        t = kv_layer(l, 512, 4, 4, 128)
+        assert sha(t["keys"].numpy()) == g[f"layer_{l:02d}"]["keys"]
+        assert sha(t["values"].numpy()) == g[f"layer_{l:02d}"]["values"]
+
+
+@pytest.mark.parametrize("layer,head", [(0, 0), (8, 3), (31, 7)])
+def test_synthetic_llama_shape_bit_exact(golden_dir, layer, head):
+    g = json.loads((golden_dir / "synthetic.json").read_text())
+    if "s2048" not in g:
+        pytest.skip("s2048 hashes not generated yet")
+    k, v = kv_slice(layer, head, seq_len=2048)
+    assert sha(k.numpy()) == g["s2048"][f"layer_{layer:02d}"]["keys"][head]
+    assert sha(v.numpy()) == g["s2048"][f"layer_{layer:02d}"]["values"][head]
+
+
+def test_extract_writes_reference_layout(tmp_path):
+    from nerf_attention import extract_kv_cache_synthetic
+    meta = extract_kv_cache_synthetic(seq_len=64, num_layers=2, num_kv_heads=2, head_dim=64,
+                                      output_dir=tmp_path)
+    d = json.loads((tmp_path / "metadata.json").read_text())
+    assert d == {"model_name": "synthetic", "num_layers": 2, "num_kv_heads": 2, "seq_len": 64,
+                 "head_dim": 64, "actual_tokens": 64, "dtype": "float32"}
+    assert types.KVMetadata.from_dict(d) == meta
+    t = torch.load(tmp_path / "layer_01.pt", weights_only=True)
+    assert t["keys"].shape == (2, 64, 64) and t["values"].dtype == torch.float32
+
+
+def test_adam_schedule():
+    tab = schedule.adam_table(2000, 1e-4)
+    lrs = schedule.lr_sequence(2000, 1e-4)
+    assert lrs[0] == 1e-4 and abs(lrs[-1] - 1e-6) < 1e-8
+    # closed form of the cosine schedule, to rounding
+    e = np.arange(2000)
+    closed = 1e-6 + 0.5 * (1e-4 - 1e-6) * (1 + np.cos(np.pi * e / 2000))
+    np.testing.assert_allclose(lrs, closed, rtol=1e-9)
+    t = e + 1.0
+    np.testing.assert_array_equal(tab[:, 0], np.float32(np.array(lrs) / (1 - 0.9 ** t)))
+    np.testing.assert_array_equal(tab[:, 1], np.float32((1 - 0.999 ** t) ** 0.5))
+
+
+def test_selection_and_order(golden_dir):
+    """Quick-mode plan names/order equal the reference run's records."""
+    ref = json.loads((golden_dir / "schema_quick" / "fit_results.json").read_text())
+    meta = types.KVMetadata("synthetic", 4, 4, 512, 128, 512)
+    layers, heads, cfgs = select_fits(meta, quick=True)
+    plan, skipped = sweep_plan(layers, heads, cfgs,
+                               lambda l: {"keys": torch.zeros(1, 8, 4),
+                                          "values": torch.zeros(1, 8, 4)})
+    assert [p[0] for p in plan] == [r["name"] for r in ref] and not skipped
+    full = types.KVMetadata("x", 32, 8, 2048, 128, 2048)
+    layers, heads, cfgs = select_fits(full, quick=False)
+    assert layers == [0, 8, 16, 24, 31] and heads == 4 and len(cfgs) == 7
+
+
+def test_missing_layer_skipped():
+    meta = types.KVMetadata("x", 4, 1, 8, 4, 8)
+    layers, heads, cfgs = select_fits(meta, quick=True)
+    plan, skipped = sweep_plan(layers, heads, cfgs,
+                               lambda l: None if l == 2 else {"keys": torch.zeros(1, 8, 4),
+                                                              "values": torch.zeros(1, 8, 4)})
+    assert skipped == [2] and all(p[1] != 2 for p in plan)
+
+
+def _fake_output(cfg, N=16, D=8):
+    torch.manual_seed(1)
+    m = SIREN(cfg, D)
+    out = engine.FitOutput(params=m.flat_parameters(), target_mean=torch.zeros(1, D),
+                           target_std=torch.ones(1, D), losses=[1.0, 0.5],
+                           row_cos=np.linspace(0.5, 1, N, dtype=np.float32),
+                           row_mse=np.ones(N, np.float32), final_mse=0.25)
+    return m, out
+
+
+def test_record_and_checkpoint_schema(golden_dir, tmp_path):
+    ref = json.loads((golden_dir / "schema_quick" / "fit_results.json").read_text())
+    layout = json.loads((golden_dir / "schema_quick" / "checkpoint_layout.json").read_text())
+    assert list(ref[0].keys()) == list(RECORD_KEYS)
+    cfg = SIRENConfig(256, 2, 30.0, "medium")
+    m, out = _fake_output(cfg, N=16, D=128)
+    res = _finish(m, cfg, out, 16, 128)
+    rec = _result_to_record("L0_H0_key_medium", 0, 0, "key", res)
+    assert list(rec.keys()) == list(ref[0].keys())
+    assert rec["num_parameters"] == 164992 and rec["raw_size_bytes"] == 16 * 128 * 2
+    assert rec["final_cosine_std"] == pytest.approx(float(np.std(out.row_cos, ddof=1)), rel=1e-5)
+    _save_model(tmp_path, "L0_H0_key_medium", res, rec)
+    ck = torch.load(tmp_path / "L0_H0_key_medium_model.pt", weights_only=True)
+    assert list(ck.keys()) == layout["top_keys"]
+    assert list(ck["model_state"].keys()) == layout["model_state_keys"]
+    assert {k: list(v.shape) for k, v in ck["model_state"].items()} == \
+        layout["model_state_shapes"]
+    assert ck["config"] == layout["config"]
+    assert list(ck["metrics"].keys()) == layout["metrics_keys"]
+
+
+def test_flat_parameter_roundtrip():
+    cfg = SIRENConfig(64, 2, 30.0, "x")
+    torch.manual_seed(3)
+    a = SIREN(cfg, 64)
+    b = SIREN(cfg, 64)
+    b.load_flat_parameters(a.flat_parameters())
+    x = torch.rand(10, 1)
+    assert torch.equal(a(x), b(x))
+
+
+def test_lpt_partition_balances():
+    cfg = {c.name: c for c in CONFIGS_FULL}
+    costs = [engine.fit_flops(2048, 128, c, 2000) for c in CONFIGS_FULL] * 40
+    for n in (1, 2, 4, 8):
+        own = engine.lpt_partition(costs, n)
+        loads = [sum(c for c, o in zip(costs, own) if o == r) for r in range(n)]
+        assert sorted(set(own)) == list(range(n))
+        assert max(loads) / (sum(costs) / n) < 1.02
+    assert engine.fit_flops(2048, 128, cfg["medium"], 2000) == pytest.approx(4.03e12, rel=1e-2)
+
+
+def test_plan_groups_by_width():
+    cfgs = [SIRENConfig(256, 2, 30.0, "m"), SIRENConfig(64, 1, 30.0, "t"),
+            SIRENConfig(256, 3, 30.0, "d"), SIRENConfig(256, 2, 60.0, "h")]
+    specs = [engine.FitSpec(torch.zeros(128, 128), c, torch.zeros(1)) for c in cfgs]
+    groups = engine.plan_groups(specs, [0])
+    assert sorted(sorted(m) for _, m in groups) == [[0, 2, 3], [1]]
+    assert groups[0][1] == [0, 2, 3]          # heaviest first
+
+
+def test_cpu_device_raises():
+    from nerf_attention import fit_siren
+    from nerf_attention._native import NerfhipError
+    with pytest.raises(NerfhipError, match="no CPU"):
+        fit_siren(torch.zeros(64, 64), SIRENConfig(64, 1, 30.0, "t"), epochs=1, device="cpu",
+                  verbose=False)
