@@ -38,9 +38,9 @@ def test_oracle_steps_bit_exact(golden_dir, name):
     torch.manual_seed(0)
     init = O.init_params(W, L, om, t.shape[1])
     assert np.array_equal(init.numpy(), z["init"])          # RNG replay of SIREN.__init__
-    r = O.fit(t, W, L, om, init, 10, record_params_at=(1, 2, 3, 10))
-    for k in (1, 2, 3):
-        assert np.array_equal(r["snapshots"][k].numpy(), z[f"params_{k}"])
+    # step 1 uses lr_0 = 1e-4 whatever T_max is: a snapshot of a longer run matches
+    r = O.fit(t, W, L, om, init, 10, record_params_at=(1,))
+    assert np.array_equal(r["snapshots"][1].numpy(), z["params_1"])
     for k in (1, 2, 3, 10):
         # T_max = k changes the schedule after step 1: rerun with epochs = k
         rk = O.fit(t, W, L, om, init, k)
