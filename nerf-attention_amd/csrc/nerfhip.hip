@@ -23,10 +23,12 @@
 // The reduction over seq_len therefore happens inside one workgroup: no
 // partial-gradient slabs, no atomics, fully deterministic.
 //
-// Scratch layout per fit (fp32, n_pad = seq_len rounded up to 64):
-//   H_i^T  [L_max+1][W][n_pad]   activations (input of linear layer i+1)
-//   dZ_i^T [L_max+1][W][n_pad]   grad at the pre-activation of sine layer i
-//   G^T    [D][n_pad]            grad at the output (2(ŷ−y)/(N·D))
+// Scratch layout per fit (fp32, n_pad = seq_len rounded up to 64), all
+// row-block-major: 16-row blocks, inside a block feature-major with the 16
+// rows contiguous (64 B per feature):
+//   H_i    [L_max+1][n_pad/16][W][16]  activations (input of linear layer i+1)
+//   dZ_i   [L_max+1][n_pad/16][W][16]  grad at the pre-activation of layer i
+//   G      [n_pad/16][D][16]           grad at the output (2(ŷ−y)/(N·D))
 //   cos_i  [L_max+1][n_pad/16][W/16][64][4]  cos(ω z), MFMA-fragment order
 //
 // Numerics: all fp32, inline ≈1-ulp sincos, f32-input MFMA = exact k-ordered
@@ -149,14 +151,109 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 // ---------------------------------------------------------------------------
 // Row-parallel step: forward + loss + backward dX chain for 64 rows of a fit.
 // mode 0 = train step; mode 1 = forward only (writes ŷ to y_out).
+//
+// Each GEMM phase streams its weight matrix through LDS in 16-row chunks,
+// double-buffered: the whole workgroup loads chunk j+1 (coalesced 16-B global
+// loads into registers) while its four waves run chunk j's MFMAs from LDS, so
+// the L2 latency of the weights hides behind ≈2K cycles of MFMA per chunk and
+// the four waves (64 rows) share one copy of every weight.  Per-lane epilogue
+// operands (targets, cos) are issued at the top of the chunk for the same
+// reason.  Rows of the LDS chunk are padded by 16 B so the lanes of one
+// ds_read_b128 (16 rows × 4 k) hit distinct banks.
 // ---------------------------------------------------------------------------
+
+// Stream rows [0, 16·JT) of `src` (row-major, row length K) through LDS and
+// compute, for every 16-row chunk J, acc = src[16J..16J+15][:] · B where the
+// B operand is the register tile b[K/16][4] (lane (c, g) holds B[16kt+4g+s][c]).
+// pre(J) runs at the top of chunk J (issue per-lane loads), epi(J, acc, pre)
+// after its MFMAs.  Ends with a barrier, so `lds` is free afterwards.
+template <int K, int JT, class Pre, class Epi>
+__device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float* lds,
+                                           const float (&b)[K / 16][4], int tid, int c, int g,
+                                           Pre&& pre, Epi&& epi) {
+  constexpr int LD = K + 4, CH = 16 * LD, NPT = K / 64, C4 = K / 4;
+  f4 st[NPT];
+#pragma unroll
+  for (int m = 0; m < NPT; ++m) {
+    const int i = tid + 256 * m;
+    st[m] = ld4(src + (i / C4) * K + (i % C4) * 4);
+  }
+#pragma unroll
+  for (int m = 0; m < NPT; ++m) {
+    const int i = tid + 256 * m;
+    st4(lds + (i / C4) * LD + (i % C4) * 4, st[m]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int J = 0; J < JT; ++J) {
+    if (J + 1 < JT) {
+      const float* nsrc = src + (J + 1) * 16 * K;
+#pragma unroll
+      for (int m = 0; m < NPT; ++m) {
+        const int i = tid + 256 * m;
+        st[m] = ld4(nsrc + (i / C4) * K + (i % C4) * 4);
+      }
+    }
+    const f4 pv = pre(J);
+    const float* buf = lds + (J & 1) * CH + c * LD + 4 * g;
+    // A fragments read two k-steps ahead; the sched_barrier keeps the
+    // compiler from hoisting every ds_read (and its registers) to the top.
+    f4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f4 a_cur = ld4(buf), a_nxt = ld4(buf + 16);
+#pragma unroll
+    for (int kt = 0; kt < K / 16; ++kt) {
+      const f4 a_n2 = ld4(buf + 16 * ((kt + 2 < K / 16) ? kt + 2 : kt));
+      f4& ac = acc[kt & 1];
+      ac = mfma16(a_cur[0], b[kt][0], ac);
+      ac = mfma16(a_cur[1], b[kt][1], ac);
+      ac = mfma16(a_cur[2], b[kt][2], ac);
+      ac = mfma16(a_cur[3], b[kt][3], ac);
+      __builtin_amdgcn_sched_barrier(0);
+      a_cur = a_nxt;
+      a_nxt = a_n2;
+    }
+    epi(J, acc[0] + acc[1], pv);
+    if (J + 1 < JT) {
+      float* nbuf = lds + ((J + 1) & 1) * CH;
+#pragma unroll
+      for (int m = 0; m < NPT; ++m) {
+        const int i = tid + 256 * m;
+        st4(nbuf + (i / C4) * LD + (i % C4) * 4, st[m]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// copy n floats (n % 4 == 0, n ≤ 1024) global → LDS, cooperatively
+__device__ __forceinline__ void stage_vec(float* dst, const float* src, int n, int tid) {
+  if (4 * tid < n) st4(dst + 4 * tid, ld4(src + 4 * tid));
+}
+
+// Output width split: a W-wide layer output is produced in NSPLIT passes of
+// W/NSPLIT features; all passes but the last park their fragments in a
+// per-wave LDS stash.  Live output registers drop from W/4 to W/(4·NSPLIT),
+// which is what lets W = 512 fit the 256 VALU-addressable VGPRs and W = 256
+// run two waves per SIMD.
+template <int W> struct RowsCfg {
+  static constexpr int NSPLIT = W >= 256 ? 2 : 1;
+  static constexpr int WAVES_PER_SIMD = W >= 512 ? 1 : 2;
+};
+
 template <int W, int D>
-__global__ void __launch_bounds__(kThreads, (W >= 256 ? 1 : 2)) k_step_rows(KArgs a) {
-  constexpr int JW = W / 16, JD = D / 16;
+__global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_rows(KArgs a) {
+  constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
+  constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
+  constexpr int WBUF = 2 * 16 * (KMAX + 4);                 // weight double buffer
+  constexpr int STASH = (NS - 1) * JP * 256;                // per wave
+  __shared__ __attribute__((aligned(16))) float lds[WBUF + KMAX + 4 * STASH];
+  float* bias = lds + WBUF;
   int fit, tile;
   if (!map_block(blockIdx.x, a.n_fits, a.n_pad / kRowsPerBlock, fit, tile)) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
+  float* stash = lds + WBUF + KMAX + wave * STASH + lane * 4;
   const int L = a.fit_layers[fit];
   const float om = a.fit_omega[fit];
   const int n_pad = a.n_pad;
@@ -173,17 +270,57 @@ __global__ void __launch_bounds__(kThreads, (W >= 256 ? 1 : 2)) k_step_rows(KArg
   float* SZ = S + (int64_t)(a.L_max + 1) * WN;
   float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
   float* SC = SG + (int64_t)D * n_pad;
+  // per-lane bases into the row-block-major [n_pad/16][F][16] scratch: the
+  // element (feature 16J+4g+q, row r) sits at +(16J+q)·16 (compile-time)
+  float* SHb = SH + (int64_t)rblk * W * 16 + g * 64 + c;
+  float* SZb = SZ + (int64_t)rblk * W * 16 + g * 64 + c;
+  float* SGb = SG + (int64_t)rblk * D * 16 + g * 64 + c;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  auto no_pre = [&](int) { return zero4; };
 
-  float hp[JW][4], hc[JW][4];
+  float hp[JW][4];      // the layer input (B operand), all W features
+  float ho[JP][4];      // one pass of the layer output
+
+  // Run a W-wide output layer as NS passes over src rows; out(Jg, acc, pv)
+  // writes feature tile Jg into ho[Jg % JP]; afterwards hp ← output.
+  auto wide_layer = [&](const float* src, auto& bop, auto&& pre, auto&& out) {
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      gemm_phase<(sizeof(bop) / sizeof(bop[0])) * 16, JP>(
+          src + (int64_t)p * JP * 16 * (sizeof(bop) / sizeof(bop[0])) * 16, lds, bop, tid, c,
+          g, [&](int J) { return pre(p * JP + J); },
+          [&](int J, f4 acc, f4 pv) { out(p * JP + J, acc, pv); });
+      if (p + 1 < NS) {
+#pragma unroll
+        for (int J = 0; J < JP; ++J) {
+          const f4 v = {ho[J][0], ho[J][1], ho[J][2], ho[J][3]};
+          st4(stash + (p * JP + J) * 256, v);
+        }
+      }
+    }
+    // all passes done (gemm_phase ended with a barrier): assemble hp
+#pragma unroll
+    for (int p = 0; p + 1 < NS; ++p)
+#pragma unroll
+      for (int J = 0; J < JP; ++J) {
+        const f4 v = ld4(stash + (p * JP + J) * 256);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hp[p * JP + J][q] = v[q];
+      }
+#pragma unroll
+    for (int J = 0; J < JP; ++J)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hp[(NS - 1) * JP + J][q] = ho[J][q];
+  };
 
   // ---- layer 0: SineLayer(1, W, is_first) — K = 1, an outer product (VALU)
+  stage_vec(lds, P, 2 * W, tid);              // w0 ‖ b0
+  __syncthreads();
   {
     const float x = a.pos[r];
-    const float* w0 = P;
-    const float* b0 = P + W;
 #pragma unroll
     for (int J = 0; J < JW; ++J) {
-      const f4 w = ld4(w0 + 16 * J + 4 * g), b = ld4(b0 + 16 * J + 4 * g);
+      const f4 w = ld4(lds + 16 * J + 4 * g), b = ld4(lds + W + 16 * J + 4 * g);
       f4 cs;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -196,170 +333,244 @@ __global__ void __launch_bounds__(kThreads, (W >= 256 ? 1 : 2)) k_step_rows(KArg
       if (train) {
         st4(SC + ((int64_t)rblk * JW + J) * 256 + lane * 4, cs);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) SH[(int64_t)(16 * J + 4 * g + q) * n_pad + r] = hp[J][q];
+        for (int q = 0; q < 4; ++q) SHb[(16 * J + q) * 16] = hp[J][q];
       }
     }
   }
+  __syncthreads();
 
   // ---- hidden SineLayers 1..L: Zᵀ = Wᵢ·Hᵀ (+b), H = sin(ω Z)
   for (int i = 1; i <= L; ++i) {
     const float* Wi = P + off_hidden_w(W, i);
-    const float* bi = Wi + W * W;
-#pragma unroll
-    for (int J = 0; J < JW; ++J) {
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* wrow = Wi + (16 * J + c) * W + 4 * g;
-#pragma unroll
-      for (int kt = 0; kt < JW; ++kt) {
-        const f4 wa = ld4(wrow + 16 * kt);
-        acc = mfma16(wa[0], hp[kt][0], acc);
-        acc = mfma16(wa[1], hp[kt][1], acc);
-        acc = mfma16(wa[2], hp[kt][2], acc);
-        acc = mfma16(wa[3], hp[kt][3], acc);
-      }
-      const f4 b = ld4(bi + 16 * J + 4 * g);
+    stage_vec(bias, Wi + W * W, W, tid);
+    float* SHi = SHb + (int64_t)i * WN;
+    float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
+    wide_layer(Wi, hp, no_pre, [&](int J, f4 acc, f4) {
+      const f4 bb = ld4(bias + 16 * J + 4 * g);
       f4 cs;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float z = __fadd_rn(acc[q], b[q]);
+        const float z = __fadd_rn(acc[q], bb[q]);
         float s, co;
         sincos_fast(__fmul_rn(om, z), &s, &co);
-        hc[J][q] = s;
+        ho[J % JP][q] = s;
         cs[q] = co;
       }
       if (train) {
-        st4(SC + (int64_t)i * WN + ((int64_t)rblk * JW + J) * 256 + lane * 4, cs);
+        st4(SCi + J * 256, cs);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          SH[(int64_t)i * WN + (int64_t)(16 * J + 4 * g + q) * n_pad + r] = hc[J][q];
+        for (int q = 0; q < 4; ++q) SHi[(16 * J + q) * 16] = ho[J % JP][q];
       }
-    }
-#pragma unroll
-    for (int J = 0; J < JW; ++J)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) hp[J][q] = hc[J][q];
+    });
   }
 
-  // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f
+  // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f ; MSE ; dL/dŷ
   const float* Wf = P + off_final_w(W, L);
-  const float* bfp = Wf + W * D;
-  f4 y[JD];
+  stage_vec(bias, Wf + W * D, D, tid);
+  const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + 4 * g;
+  float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + 4 * g : nullptr;
+  float y[JD][4];
+  float sq = 0.f;
+  gemm_phase<W, JD>(
+      Wf, lds, hp, tid, c, g,
+      [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
+      [&](int J, f4 acc, f4 t) {
+        const f4 bb = ld4(bias + 16 * J + 4 * g);
+        f4 yv;
 #pragma unroll
-  for (int J = 0; J < JD; ++J) {
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wrow = Wf + (16 * J + c) * W + 4 * g;
+        for (int q = 0; q < 4; ++q) yv[q] = __fadd_rn(acc[q], bb[q]);
+        if (yo) st4(yo + 16 * J, yv);             // lane holds ŷ[r][16J+4g+q]
+        if (train) {
 #pragma unroll
-    for (int kt = 0; kt < JW; ++kt) {
-      const f4 wa = ld4(wrow + 16 * kt);
-      acc = mfma16(wa[0], hp[kt][0], acc);
-      acc = mfma16(wa[1], hp[kt][1], acc);
-      acc = mfma16(wa[2], hp[kt][2], acc);
-      acc = mfma16(wa[3], hp[kt][3], acc);
-    }
-    const f4 b = ld4(bfp + 16 * J + 4 * g);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) y[J][q] = __fadd_rn(acc[q], b[q]);
-  }
-  if (a.y_out) {
-    float* yo = a.y_out + fit * a.y_stride + (int64_t)r * D;
-#pragma unroll
-    for (int J = 0; J < JD; ++J) {
-      // lane holds ŷ[r][16J+4g+q]: one 16-B store per J
-      st4(yo + 16 * J + 4 * g, y[J]);
-    }
-  }
+          for (int q = 0; q < 4; ++q) {
+            const float diff = yv[q] - t[q];
+            sq = valid ? fmaf(diff, diff, sq) : sq;
+            const float gr = valid ? a.grad_scale * diff : 0.f;
+            y[J][q] = gr;
+            SGb[(16 * J + q) * 16] = gr;
+          }
+        }
+      });
   if (!train) return;
+  sq = wave_sum(sq);
+  if (lane == 0)
+    a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] = sq;
 
-  // ---- MSE (F.mse_loss, reduction mean) and its gradient 2(ŷ−y)/numel
-  {
-    const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D;
-    float sq = 0.f;
-#pragma unroll
-    for (int J = 0; J < JD; ++J) {
-      const f4 t = ld4(T + 16 * J + 4 * g);
+  // ---- backward.  Each epilogue turns its dH tile into dZ = (dH ⊙ cos(ωz))·ω
+  // right away (the next phase's B operand) and stores it for the weight grads.
+  auto dz_out = [&](int layer) {
+    float* SZl = SZb + (int64_t)layer * WN;
+    return [&, SZl](int K, f4 acc, f4 cs) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float diff = y[J][q] - t[q];
-        sq = valid ? fmaf(diff, diff, sq) : sq;
-        const float gr = valid ? a.grad_scale * diff : 0.f;
-        y[J][q] = gr;
-        SG[(int64_t)(16 * J + 4 * g + q) * n_pad + r] = gr;
+        const float dz = __fmul_rn(__fmul_rn(acc[q], cs[q]), om);
+        ho[K % JP][q] = dz;
+        SZl[(16 * K + q) * 16] = dz;
       }
-    }
-    sq = wave_sum(sq);
-    if (lane == 0)
-      a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] = sq;
-  }
-
-  // ---- backward: dH_Lᵀ = W_fᵀ·Gᵀ
-  float dh[JW][4];
-  {
-    const float* WfT = PT + (int64_t)L * W * W;  // [W][D]
-#pragma unroll
-    for (int K = 0; K < JW; ++K) {
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* wrow = WfT + (16 * K + c) * D + 4 * g;
-#pragma unroll
-      for (int J = 0; J < JD; ++J) {
-        const f4 wa = ld4(wrow + 16 * J);
-        acc = mfma16(wa[0], y[J][0], acc);
-        acc = mfma16(wa[1], y[J][1], acc);
-        acc = mfma16(wa[2], y[J][2], acc);
-        acc = mfma16(wa[3], y[J][3], acc);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dh[K][q] = acc[q];
-    }
-  }
-
-  // ---- sine layers L..0: dZ = (dH ⊙ cos(ωz))·ω ; dH_prevᵀ = Wᵢᵀ·dZᵀ
-  for (int i = L; i >= 0; --i) {
-    const float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
-    float* SZi = SZ + (int64_t)i * WN;
-#pragma unroll
-    for (int K = 0; K < JW; ++K) {
-      const f4 cs = ld4(SCi + K * 256);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float dz = __fmul_rn(__fmul_rn(dh[K][q], cs[q]), om);
-        hc[K][q] = dz;
-        SZi[(int64_t)(16 * K + 4 * g + q) * n_pad + r] = dz;
-      }
-    }
-    if (i == 0) break;
-    const float* WiT = PT + (int64_t)(i - 1) * W * W;  // [W_in][W_out]
-#pragma unroll
-    for (int K = 0; K < JW; ++K) {
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* wrow = WiT + (16 * K + c) * W + 4 * g;
-#pragma unroll
-      for (int J = 0; J < JW; ++J) {
-        const f4 wa = ld4(wrow + 16 * J);
-        acc = mfma16(wa[0], hc[J][0], acc);
-        acc = mfma16(wa[1], hc[J][1], acc);
-        acc = mfma16(wa[2], hc[J][2], acc);
-        acc = mfma16(wa[3], hc[J][3], acc);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dh[K][q] = acc[q];
-    }
-  }
+    };
+  };
+  auto cos_pre = [&](int layer) {
+    const float* SCl = SC + (int64_t)layer * WN + (int64_t)rblk * JW * 256 + lane * 4;
+    return [SCl](int K) { return ld4(SCl + K * 256); };
+  };
+  wide_layer(PT + (int64_t)L * W * W, y, cos_pre(L), dz_out(L));   // W_fᵀ [W][D]
+  for (int i = L; i >= 1; --i)
+    wide_layer(PT + (int64_t)(i - 1) * W * W, hp, cos_pre(i - 1), dz_out(i - 1));
 }
 
 // ---------------------------------------------------------------------------
 // Parameter-parallel step: weight/bias gradients reduced over all rows, then
-// Adam.  Tiles per fit: L·(W/64)² hidden + (D/64)(W/64) final + W/64 first.
+// Adam.  Tiles per fit: L·(W/T)² hidden + (D/TD)(W/T) final + W/64 first.
+//
+// A tile dW[j0:j0+TJ][k0:k0+TK] = Σ_r dZ[r][j]·H[r][k] streams the two
+// operands 16 rows at a time: each 16-row block of a 128-feature slice is one
+// contiguous 8 KB run of the row-block-major scratch.  Blocks go global →
+// registers (two blocks in flight) → padded LDS (feature stride 20 floats:
+// conflict-free ds_read_b128) → v_mfma_f32_32x32x2_f32, whose k index walks
+// the 16 rows as 8h+s so each lane reads its 8 rows with two ds_read_b128.
 // ---------------------------------------------------------------------------
+constexpr int kFs = 20;  // LDS floats per feature per 16-row block (16 + pad)
+
+template <int TJ, int TK>
+__device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict__ A, int FA,
+                                        const float* __restrict__ B, int FB, int j0, int k0,
+                                        float* P, float* M, float* V, float* PT, int64_t pw,
+                                        int64_t pb, int64_t ptw, int out_dim, bool do_bias_tile,
+                                        float step_size, float bc2s, float* lds) {
+  constexpr int NA = TJ / 64, NB = TK / 64;            // 32×32 MFMA tiles per wave
+  constexpr int NPT = (TJ + TK) / 64;                  // f4 per thread per block
+  constexpr int BUF = (TJ + TK) * kFs;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wj = wave >> 1, wk = wave & 1, h = lane >> 5, lr = lane & 31;
+  const int n_blocks = a.n_pad / 16;
+  const float* Ab = A + (int64_t)j0 * 16;
+  const float* Bb = B + (int64_t)k0 * 16;
+  const int64_t sA = (int64_t)FA * 16, sB = (int64_t)FB * 16;
+
+  auto gload = [&](f4 (&st)[NPT], int rb) {
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + 256 * m;
+      st[m] = (i < TJ * 4) ? ld4(Ab + rb * sA + i * 4) : ld4(Bb + rb * sB + (i - TJ * 4) * 4);
+    }
+  };
+  auto lstore = [&](const f4 (&st)[NPT], float* buf) {
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + 256 * m;           // feature i/4, quarter i%4 (A then B)
+      st4(buf + (i >> 2) * kFs + (i & 3) * 4, st[m]);
+    }
+  };
+
+  f16v acc[NA][NB];
+#pragma unroll
+  for (int x = 0; x < NA; ++x)
+#pragma unroll
+    for (int y = 0; y < NB; ++y)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[x][y][q] = 0.f;
+  float bsum[NA];
+#pragma unroll
+  for (int x = 0; x < NA; ++x) bsum[x] = 0.f;
+  const bool do_bias = do_bias_tile && wk == 0;
+
+  f4 st0[NPT], st1[NPT];
+  gload(st0, 0);
+  lstore(st0, lds);
+  if (n_blocks > 1) gload(st1, 1);
+  __syncthreads();
+  const float* a_base = lds + (wj * (TJ / 2) + lr) * kFs + 8 * h;
+  const float* b_base = lds + (TJ + wk * (TK / 2) + lr) * kFs + 8 * h;
+
+  auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
+    // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
+    if (rb + 2 < n_blocks) gload(st_next, rb + 2);
+    const int off = (rb & 1) * BUF;
+    f4 av[NA][2], bv[NB][2];
+#pragma unroll
+    for (int x = 0; x < NA; ++x) {
+      av[x][0] = ld4(a_base + off + x * 32 * kFs);
+      av[x][1] = ld4(a_base + off + x * 32 * kFs + 4);
+    }
+#pragma unroll
+    for (int y = 0; y < NB; ++y) {
+      bv[y][0] = ld4(b_base + off + y * 32 * kFs);
+      bv[y][1] = ld4(b_base + off + y * 32 * kFs + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int x = 0; x < NA; ++x)
+#pragma unroll
+        for (int y = 0; y < NB; ++y)
+          acc[x][y] = mfma32(av[x][s >> 2][s & 3], bv[y][s >> 2][s & 3], acc[x][y]);
+    if (do_bias) {
+#pragma unroll
+      for (int x = 0; x < NA; ++x)
+        bsum[x] += ((av[x][0][0] + av[x][0][1]) + (av[x][0][2] + av[x][0][3])) +
+                   ((av[x][1][0] + av[x][1][1]) + (av[x][1][2] + av[x][1][3]));
+    }
+    if (rb + 1 < n_blocks) lstore(st_fill, lds + ((rb + 1) & 1) * BUF);
+    __syncthreads();
+  };
+  for (int rb = 0; rb < n_blocks; rb += 2) {
+    block(rb, st0, st1);
+    if (rb + 1 < n_blocks) block(rb + 1, st1, st0);
+  }
+
+  // Adam on the wave's (TJ/2)×(TK/2) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
+#pragma unroll
+  for (int x = 0; x < NA; ++x)
+#pragma unroll
+    for (int y = 0; y < NB; ++y) {
+      const int jrow0 = j0 + wj * (TJ / 2) + 32 * x;
+      const int kcol = k0 + wk * (TK / 2) + 32 * y + lr;
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) {
+        f4 pt;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int j = jrow0 + qq + 8 * qb + 4 * h;
+          const int64_t idx = pw + (int64_t)j * a.W + kcol;
+          float p = P[idx], mm = M[idx], vv = V[idx];
+          adam_update(p, mm, vv, acc[x][y][qb * 4 + qq], step_size, bc2s);
+          P[idx] = p; M[idx] = mm; V[idx] = vv;
+          pt[qq] = p;
+        }
+        st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int x = 0; x < NA; ++x) {
+      const float s = bsum[x] + __shfl_xor(bsum[x], 32, 64);
+      if (h == 0) {
+        const int64_t idx = pb + j0 + wj * (TJ / 2) + 32 * x + lr;
+        float p = P[idx], mm = M[idx], vv = V[idx];
+        adam_update(p, mm, vv, s, step_size, bc2s);
+        P[idx] = p; M[idx] = mm; V[idx] = vv;
+      }
+    }
+  }
+}
+
+template <int W, int D> struct ParamsCfg {
+  static constexpr int T = W < 128 ? W : 128;          // hidden-layer tile (both dims)
+  static constexpr int TD = D < T ? D : T;             // final-layer tile rows
+  static constexpr int NT = W / T;
+  static constexpr int TH = NT * NT, TF = (D / TD) * NT, T0 = W / 64;
+  __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
+};
+
 template <int W, int D>
-__global__ void __launch_bounds__(kThreads) k_step_params(KArgs a) {
-  constexpr int WT = W / 64;
-  constexpr int TH = WT * WT, TF = (D / 64) * WT, T0 = WT;
-  const int n_tiles_max = a.L_max * TH + TF + T0;
+__global__ void __launch_bounds__(kThreads, 2) k_step_params(KArgs a) {
+  using C = ParamsCfg<W, D>;
+  __shared__ __attribute__((aligned(16))) float lds[2 * (2 * C::T) * kFs];
   int fit, t;
-  if (!map_block(blockIdx.x, a.n_fits, n_tiles_max, fit, t)) return;
+  if (!map_block(blockIdx.x, a.n_fits, C::tiles(a.L_max), fit, t)) return;
   const int L = a.fit_layers[fit];
-  if (t >= L * TH + TF + T0) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (t >= C::tiles(L)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n_pad = a.n_pad;
   const float step_size = a.sched[2 * a.epoch], bc2s = a.sched[2 * a.epoch + 1];
 
@@ -373,99 +584,45 @@ __global__ void __launch_bounds__(kThreads) k_step_params(KArgs a) {
   const float* SZ = S + (int64_t)(a.L_max + 1) * WN;
   const float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
 
-  if (t < L * TH + TF) {
-    const float *Asrc, *Bsrc;
-    int out_dim, tj, tk;
-    int64_t pw, pb, ptw;
-    if (t < L * TH) {
-      const int layer = t / TH + 1, u = t % TH;
-      tj = u / WT; tk = u % WT;
-      Asrc = SZ + (int64_t)layer * WN;
-      Bsrc = SH + (int64_t)(layer - 1) * WN;
-      out_dim = W;
-      pw = off_hidden_w(W, layer);
-      pb = pw + (int64_t)W * W;
-      ptw = (int64_t)(layer - 1) * W * W;
-    } else {
-      const int u = t - L * TH;
-      tj = u / WT; tk = u % WT;
-      Asrc = SG;
-      Bsrc = SH + (int64_t)L * WN;
-      out_dim = D;
-      pw = off_final_w(W, L);
-      pb = pw + (int64_t)W * D;
-      ptw = (int64_t)L * W * W;
-    }
-    const int wj = wave >> 1, wk = wave & 1;
-    const int h = lane >> 5, lr = lane & 31;
-    const int jrow0 = tj * 64 + wj * 32;
-    const int kcol = tk * 64 + wk * 32 + lr;
-    const float* ap = Asrc + (int64_t)(jrow0 + lr) * n_pad + 4 * h;
-    const float* bp = Bsrc + (int64_t)kcol * n_pad + 4 * h;
-    f16v acc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-    float bsum = 0.f;
-    const bool do_bias = (tk == 0) && (wk == 0);
-    f4 av = ld4(ap), bv = ld4(bp);
-    for (int rb = 0; rb < n_pad; rb += 8) {
-      const int nx = (rb + 8 < n_pad) ? rb + 8 : rb;
-      const f4 an = ld4(ap + nx), bn = ld4(bp + nx);
-      acc = mfma32(av[0], bv[0], acc);
-      acc = mfma32(av[1], bv[1], acc);
-      acc = mfma32(av[2], bv[2], acc);
-      acc = mfma32(av[3], bv[3], acc);
-      if (do_bias) bsum += (av[0] + av[1]) + (av[2] + av[3]);
-      av = an; bv = bn;
-    }
-    // Adam on the 32×32 sub-tile; lane holds rows (q&3)+8(q>>2)+4h, col lr.
-#pragma unroll
-    for (int qb = 0; qb < 4; ++qb) {
-      f4 pt;
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int q = qb * 4 + qq;
-        const int j = jrow0 + qq + 8 * qb + 4 * h;
-        const int64_t idx = pw + (int64_t)j * W + kcol;
-        float p = P[idx], mm = M[idx], vv = V[idx];
-        adam_update(p, mm, vv, acc[q], step_size, bc2s);
-        P[idx] = p; M[idx] = mm; V[idx] = vv;
-        pt[qq] = p;
-      }
-      st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
-    }
-    if (do_bias) {
-      bsum += __shfl_xor(bsum, 32, 64);
-      if (h == 0) {
-        const int64_t idx = pb + jrow0 + lr;
-        float p = P[idx], mm = M[idx], vv = V[idx];
-        adam_update(p, mm, vv, bsum, step_size, bc2s);
-        P[idx] = p; M[idx] = mm; V[idx] = vv;
-      }
-    }
+  if (t < L * C::TH) {
+    const int layer = t / C::TH + 1, u = t % C::TH;
+    const int64_t pw = off_hidden_w(W, layer);
+    dw_tile<C::T, C::T>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN, W,
+                        (u / C::NT) * C::T, (u % C::NT) * C::T, P, M, V, PT, pw,
+                        pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
+                        (u % C::NT) == 0, step_size, bc2s, lds);
+  } else if (t < L * C::TH + C::TF) {
+    const int u = t - L * C::TH;
+    const int64_t pw = off_final_w(W, L);
+    dw_tile<C::TD, C::T>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
+                         (u % C::NT) * C::T, P, M, V, PT, pw, pw + (int64_t)W * D,
+                         (int64_t)L * W * W, D, (u % C::NT) == 0, step_size, bc2s, lds);
   } else {
-    // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0
-    const int u = t - L * TH - TF;
-    const float* pos = a.pos;
-    for (int f = 0; f < 16; ++f) {
-      const int j = u * 64 + wave * 16 + f;
-      const float* zp = SZ + (int64_t)j * n_pad;
-      float sw = 0.f, sb = 0.f;
-      for (int r4 = lane * 4; r4 < n_pad; r4 += 256) {
-        const f4 z = ld4(zp + r4), x = ld4(pos + r4);
-        sw += (z[0] * x[0] + z[1] * x[1]) + (z[2] * x[2] + z[3] * x[3]);
-        sb += (z[0] + z[1]) + (z[2] + z[3]);
-      }
-      sw = wave_sum(sw);
-      sb = wave_sum(sb);
-      if (lane == 0) {
-        float p = P[j], mm = M[j], vv = V[j];
-        adam_update(p, mm, vv, sw, step_size, bc2s);
-        P[j] = p; M[j] = mm; V[j] = vv;
-        p = P[W + j]; mm = M[W + j]; vv = V[W + j];
-        adam_update(p, mm, vv, sb, step_size, bc2s);
-        P[W + j] = p; M[W + j] = mm; V[W + j] = vv;
-      }
+    // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0.  Lane = (feature
+    // f = lane/4 of the wave's 16, quarter m = lane%4 of a 16-row block).
+    const int u = t - L * C::TH - C::TF;
+    const int f = lane >> 2, m = lane & 3;
+    const int j = u * 64 + wave * 16 + f;
+    const float* zp = SZ + (int64_t)j * 16 + 4 * m;
+    const float* xp = a.pos + 4 * m;
+    float sw = 0.f, sb = 0.f;
+#pragma unroll 4
+    for (int rb = 0; rb < n_pad / 16; ++rb) {
+      const f4 z = ld4(zp + (int64_t)rb * W * 16), x = ld4(xp + rb * 16);
+      sw += (z[0] * x[0] + z[1] * x[1]) + (z[2] * x[2] + z[3] * x[3]);
+      sb += (z[0] + z[1]) + (z[2] + z[3]);
+    }
+    sw += __shfl_xor(sw, 1, 64);
+    sw += __shfl_xor(sw, 2, 64);
+    sb += __shfl_xor(sb, 1, 64);
+    sb += __shfl_xor(sb, 2, 64);
+    if (m == 0) {
+      float p = P[j], mm = M[j], vv = V[j];
+      adam_update(p, mm, vv, sw, step_size, bc2s);
+      P[j] = p; M[j] = mm; V[j] = vv;
+      p = P[W + j]; mm = M[W + j]; vv = V[W + j];
+      adam_update(p, mm, vv, sb, step_size, bc2s);
+      P[W + j] = p; M[W + j] = mm; V[W + j] = vv;
     }
   }
 }
@@ -614,9 +771,7 @@ int launch_rows(const KArgs& a, hipStream_t st) {
 
 template <int W, int D>
 int launch_params(const KArgs& a, hipStream_t st) {
-  constexpr int WT = W / 64;
-  const int n_tiles = a.L_max * WT * WT + (D / 64) * WT + WT;
-  const int grid = grid_for(a.n_fits, n_tiles);
+  const int grid = grid_for(a.n_fits, ParamsCfg<W, D>::tiles(a.L_max));
   hipLaunchKernelGGL((k_step_params<W, D>), dim3(grid), dim3(kThreads), 0, st, a);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
