@@ -111,12 +111,6 @@ def main() -> None:
     mine = farm.rank_share(costs, world, rank)
     job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[local])
 
-    # dominant group on this rank = the one with the most FLOPs
-    g_flops = [sum(costs[mine[i]] for i in g.members) for g in job.groups]
-    tg = int(np.argmax(g_flops))
-    dom = job.groups[tg]
-    dom_cfgs = [specs[mine[i]].config for i in dom.members]
-
     for _ in range(args.warmup):
         job.launch()
         job.wait()
@@ -124,15 +118,14 @@ def main() -> None:
     barrier = farm.barrier
     barrier()
     t0 = time.perf_counter()
-    rows_ms = params_ms = 0.0
-    launches = 0
+    kt = [[0.0, 0.0, 0] for _ in job.groups]       # per group: rows ms, params ms, launches
     for _ in range(args.steps):
-        job.launch(time_group=None if args.no_kernel_timing else tg)
+        job.launch(timed=not args.no_kernel_timing)
         job.wait()
-        if job.timing is not None:
-            rows_ms += job.timing.rows_ms
-            params_ms += job.timing.params_ms
-            launches += job.timing.launches
+        for acc, t in zip(kt, job.timing or []):
+            acc[0] += t.rows_ms
+            acc[1] += t.params_ms
+            acc[2] += t.launches
     barrier()
     elapsed = time.perf_counter() - t0
     t_max = farm.max_over_ranks(elapsed)
@@ -145,23 +138,30 @@ def main() -> None:
     if rank == 0:
         value = n_total * args.steps / t_max
         roof = None
-        if launches:
+        if any(k[2] for k in kt):
+            # dominant kernel = largest summed device time over the timed steps
             N = args.seq_len
-            cand = {"k_step_rows": (rows_ms / launches, rows_flops(N, 128, dom_cfgs)),
-                    "k_step_params": (params_ms / launches, params_flops(N, 128, dom_cfgs))}
-            kname = max(cand, key=lambda k: cand[k][0])
-            avg_ms, flops = cand[kname]
+            cands = []
+            for g, (r_ms, p_ms, n) in zip(job.groups, kt):
+                cf = [specs[mine[i]].config for i in g.members]
+                cands.append((r_ms, f"k_step_rows<{g.W},128>", r_ms / n, rows_flops(N, 128, cf), g))
+                cands.append((p_ms, f"k_step_params<{g.W},128>", p_ms / n,
+                              params_flops(N, 128, cf), g))
+            _, kname, avg_ms, flops, g = max(cands, key=lambda c: c[0])
             achieved = flops / (avg_ms * 1e-3) / 1e12
             traffic = None
             if PMC_TRAFFIC.exists():
-                traffic = json.loads(PMC_TRAFFIC.read_text()).get(f"{kname}<{dom.W},128>")
+                traffic = json.loads(PMC_TRAFFIC.read_text()).get(kname)
+            step_flops = sum(engine.fit_flops(N, 128, specs[i].config, args.epochs)
+                             for i in mine)
             roof = {"bound": "mfma", "achieved": round(achieved, 3),
                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "kernel": f"{kname}<{dom.W},128>", "fits_per_launch": dom.n,
-                    "avg_launch_ms": round(avg_ms, 4),
-                    "other_kernel_avg_ms": {k: round(v[0], 4) for k, v in cand.items()
-                                            if k != kname}}
+                    "kernel": kname, "fits_per_launch": g.n, "avg_launch_ms": round(avg_ms, 4),
+                    "flops_per_launch": flops,
+                    "note": "launch durations measured while the width groups run concurrently",
+                    "kernels_avg_ms": {c[1]: round(c[2], 4) for c in cands},
+                    "job_achieved_tflops": round(step_flops / (t_max / args.steps) / 1e12, 2)}
         parity = None
         if GOLDEN_SWEEP.exists() and args.epochs == 2000 and args.seq_len == 2048:
             ref = json.loads(GOLDEN_SWEEP.read_text())["records"]

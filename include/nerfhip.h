@@ -110,19 +110,20 @@ int nerfhip_group_sizes(int32_t W, int32_t D, int32_t N, int32_t L_max, int32_t 
  * validated before anything is enqueued. */
 int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const* streams);
 
-/* Per-kernel device time of one group, measured with hipEvents bracketing
+/* Per-kernel device time of a group, measured with hipEvents bracketing
  * every launch of its two step kernels (bench.py's roofline leg). */
 typedef struct nerfhip_timing {
-  int32_t group;           /* in: index of the group to time                  */
-  int32_t launches;        /* out: timed launches per kernel (= its epochs)   */
+  int32_t launches;        /* out: timed launches per kernel (= the epochs)   */
+  int32_t reserved;
   double rows_ms;          /* out: Σ duration of the row-step launches        */
   double params_ms;        /* out: Σ duration of the parameter-step launches  */
 } nerfhip_timing;
 
-/* nerfhip_siren_fit + timing of group timing->group.  Unlike the untimed
- * call it synchronises that group's stream before returning. */
+/* nerfhip_siren_fit, with timings[i] (an array of n_groups records) filled
+ * for every group.  Unlike the untimed call it synchronises every group's
+ * stream before returning. */
 int nerfhip_siren_fit_timed(const nerfhip_group* groups, int32_t n_groups,
-                            void* const* streams, nerfhip_timing* timing);
+                            void* const* streams, nerfhip_timing* timings);
 
 /* Forward only with the current params → eval_y (+ row metrics when
  * target/mean/std/row_cos/row_sq are set).  SIREN.forward, siren.py:60-61. */

@@ -876,7 +876,7 @@ int prologue(GroupRun& r) {
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
-int epoch_step(GroupRun& r, int e) {
+int epoch_step(GroupRun& r, int e, hipEvent_t* ev /* 3 or NULL */) {
   KArgs& a = r.a;
   a.epoch = e;
   a.mode = 0;
@@ -885,8 +885,11 @@ int epoch_step(GroupRun& r, int e) {
     a.y_out = r.g->probe_y + (int64_t)((e + 1) / r.g->log_every - 1) * r.s.target;
     a.y_stride = r.probe_stride;
   }
+  if (ev) (void)hipEventRecord(ev[0], r.st);
   int rc = r.rows(a, r.st);
+  if (ev) (void)hipEventRecord(ev[1], r.st);
   if (rc == NERFHIP_OK) rc = r.params(a, r.st);
+  if (ev) (void)hipEventRecord(ev[2], r.st);
   return rc;
 }
 
@@ -922,81 +925,65 @@ GroupRun make_run(const nerfhip_group* g, void* stream) {
 }  // namespace
 
 static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* streams,
-                    nerfhip_timing* timing) {
+                    nerfhip_timing* timings) {
   if (!groups || !streams || n_groups < 1) return NERFHIP_ERR_NULL;
   for (int i = 0; i < n_groups; ++i) {
     const int rc = check_group(&groups[i], true);
     if (rc != NERFHIP_OK) return rc;
   }
-  if (timing && (timing->group < 0 || timing->group >= n_groups)) return NERFHIP_ERR_BAD_SHAPE;
   int prev = -1;
   if (hipGetDevice(&prev) != hipSuccess) return NERFHIP_ERR_LAUNCH;
   int cur = prev;
   GroupRun* runs = new GroupRun[n_groups];
+  hipEvent_t** ev = timings ? new hipEvent_t*[n_groups]() : nullptr;
   int rc = NERFHIP_OK, max_epochs = 0;
   for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
     runs[i] = make_run(&groups[i], streams[i]);
     if (groups[i].epochs > max_epochs) max_epochs = groups[i].epochs;
     rc = select_device(groups[i].device, &cur);
     if (rc == NERFHIP_OK) rc = prologue(runs[i]);
-  }
-  // timing: 3 events per epoch of the timed group (before rows, between, after params)
-  const int tg = timing ? timing->group : -1;
-  const int t_epochs = timing ? groups[tg].epochs : 0;
-  hipEvent_t* ev = nullptr;
-  if (timing && rc == NERFHIP_OK) {
-    rc = select_device(groups[tg].device, &cur);
-    ev = new hipEvent_t[3 * (size_t)t_epochs]();
-    for (int k = 0; k < 3 * t_epochs && rc == NERFHIP_OK; ++k)
-      if (hipEventCreate(&ev[k]) != hipSuccess) rc = NERFHIP_ERR_LAUNCH;
+    if (ev && rc == NERFHIP_OK) {
+      // 3 events per epoch: before the row step, between, after the param step
+      const int ne = 3 * groups[i].epochs;
+      ev[i] = new hipEvent_t[ne > 0 ? ne : 1]();
+      for (int k = 0; k < ne && rc == NERFHIP_OK; ++k)
+        if (hipEventCreate(&ev[i][k]) != hipSuccess) rc = NERFHIP_ERR_LAUNCH;
+    }
   }
   for (int e = 0; e < max_epochs && rc == NERFHIP_OK; ++e)
     for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
       if (e >= groups[i].epochs) continue;
       rc = select_device(groups[i].device, &cur);
-      if (rc != NERFHIP_OK) break;
-      if (i == tg) {
-        GroupRun& r = runs[i];
-        KArgs& a = r.a;
-        a.epoch = e;
-        a.mode = 0;
-        a.y_out = nullptr;
-        if (r.n_probe > 0 && (e + 1) % r.g->log_every == 0) {
-          a.y_out = r.g->probe_y + (int64_t)((e + 1) / r.g->log_every - 1) * r.s.target;
-          a.y_stride = r.probe_stride;
-        }
-        (void)hipEventRecord(ev[3 * e], r.st);
-        rc = r.rows(a, r.st);
-        (void)hipEventRecord(ev[3 * e + 1], r.st);
-        if (rc == NERFHIP_OK) rc = r.params(a, r.st);
-        (void)hipEventRecord(ev[3 * e + 2], r.st);
-      } else {
-        rc = epoch_step(runs[i], e);
-      }
+      if (rc == NERFHIP_OK) rc = epoch_step(runs[i], e, ev ? ev[i] + 3 * e : nullptr);
     }
   for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
     rc = select_device(groups[i].device, &cur);
     if (rc == NERFHIP_OK) rc = epilogue(runs[i]);
   }
   if (ev) {
-    if (rc == NERFHIP_OK && select_device(groups[tg].device, &cur) == NERFHIP_OK &&
-        hipStreamSynchronize(runs[tg].st) == hipSuccess) {
-      double rows_ms = 0.0, params_ms = 0.0;
-      for (int e = 0; e < t_epochs; ++e) {
-        float a = 0.f, b = 0.f;
-        (void)hipEventElapsedTime(&a, ev[3 * e], ev[3 * e + 1]);
-        (void)hipEventElapsedTime(&b, ev[3 * e + 1], ev[3 * e + 2]);
-        rows_ms += a;
-        params_ms += b;
+    for (int i = 0; i < n_groups; ++i) {
+      if (!ev[i]) continue;
+      const int E = groups[i].epochs;
+      if (rc == NERFHIP_OK) rc = select_device(groups[i].device, &cur);
+      if (rc == NERFHIP_OK && hipStreamSynchronize(runs[i].st) != hipSuccess) rc = NERFHIP_ERR_LAUNCH;
+      if (rc == NERFHIP_OK) {
+        double rows_ms = 0.0, params_ms = 0.0;
+        for (int e = 0; e < E; ++e) {
+          float x = 0.f, y = 0.f;
+          (void)hipEventElapsedTime(&x, ev[i][3 * e], ev[i][3 * e + 1]);
+          (void)hipEventElapsedTime(&y, ev[i][3 * e + 1], ev[i][3 * e + 2]);
+          rows_ms += x;
+          params_ms += y;
+        }
+        timings[i].launches = E;
+        timings[i].reserved = 0;
+        timings[i].rows_ms = rows_ms;
+        timings[i].params_ms = params_ms;
       }
-      timing->launches = t_epochs;
-      timing->rows_ms = rows_ms;
-      timing->params_ms = params_ms;
-    } else if (rc == NERFHIP_OK) {
-      rc = NERFHIP_ERR_LAUNCH;
+      for (int k = 0; k < 3 * E; ++k)
+        if (ev[i][k]) (void)hipEventDestroy(ev[i][k]);
+      delete[] ev[i];
     }
-    for (int k = 0; k < 3 * t_epochs; ++k)
-      if (ev[k]) (void)hipEventDestroy(ev[k]);
     delete[] ev;
   }
   delete[] runs;
@@ -1009,9 +996,9 @@ int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const
 }
 
 int nerfhip_siren_fit_timed(const nerfhip_group* groups, int32_t n_groups, void* const* streams,
-                            nerfhip_timing* timing) {
-  if (!timing) return NERFHIP_ERR_NULL;
-  return fit_impl(groups, n_groups, streams, timing);
+                            nerfhip_timing* timings) {
+  if (!timings) return NERFHIP_ERR_NULL;
+  return fit_impl(groups, n_groups, streams, timings);
 }
 
 int nerfhip_siren_forward(const nerfhip_group* g, void* stream) {

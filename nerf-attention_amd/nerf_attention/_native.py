@@ -43,7 +43,7 @@ class NerfhipGroup(ctypes.Structure):
 
 
 class NerfhipTiming(ctypes.Structure):
-    _fields_ = [("group", c_int32), ("launches", c_int32), ("rows_ms", ctypes.c_double),
+    _fields_ = [("launches", c_int32), ("reserved", c_int32), ("rows_ms", ctypes.c_double),
                 ("params_ms", ctypes.c_double)]
 
 

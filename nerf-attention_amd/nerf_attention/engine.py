@@ -261,23 +261,22 @@ class FitJob:
                 g.params.copy_(g.params_init, non_blocking=True)
         self.fresh = True
 
-    def launch(self, time_group: int | None = None) -> None:
-        """Enqueue every group.  time_group: index into self.groups whose two
-        step kernels get hipEvent timing (synchronises that group)."""
+    def launch(self, timed: bool = False) -> None:
+        """Enqueue every group.  timed=True brackets every step-kernel launch
+        with hipEvents (self.timing[i] per group; synchronises the groups)."""
         if not self.fresh:
             self.reset()
         self.fresh = False
         G = len(self.groups)
         for g in self.groups:
             g.ev_start.record(g.stream)
-        if time_group is None:
+        if not timed:
             _native.check(_native.load().nerfhip_siren_fit(self._descs, G, self._streams))
             self.timing = None
         else:
-            t = _native.NerfhipTiming(group=time_group)
-            _native.check(_native.load().nerfhip_siren_fit_timed(self._descs, G, self._streams,
-                                                                 ctypes.byref(t)))
-            self.timing = t
+            t = (_native.NerfhipTiming * G)()
+            _native.check(_native.load().nerfhip_siren_fit_timed(self._descs, G, self._streams, t))
+            self.timing = list(t)
         for g in self.groups:
             g.ev_end.record(g.stream)
 

@@ -75,6 +75,5 @@ def test_fit_rejects_before_touching_device(lib):
     g.W = 100
     assert lib.nerfhip_siren_fit(ctypes.byref(g), 1, streams) == -1
     assert lib.nerfhip_siren_fit(None, 1, streams) == -5
-    t = _native.NerfhipTiming(group=3)
     assert lib.nerfhip_siren_fit_timed(ctypes.byref(g), 1, streams, None) == -5
     assert lib.nerfhip_siren_forward(None, None) == -5
