@@ -19,6 +19,7 @@ from .types import (
 from .siren import SIREN, SineLayer, fit_siren
 from .synthetic import extract_kv_cache_synthetic
 from .fit import fit_kv_cache
+from . import ops  # registers torch.ops.nerfhip.*
 
 __all__ = [
     "CONFIG_WIDE", "CONFIGS_FULL", "CONFIGS_QUICK", "FitResult", "KVMetadata", "SIRENConfig",

@@ -180,3 +180,17 @@ def test_cpu_device_raises():
     with pytest.raises(NerfhipError, match="no CPU"):
         fit_siren(torch.zeros(64, 64), SIRENConfig(64, 1, 30.0, "t"), epochs=1, device="cpu",
                   verbose=False)
+
+
+def test_custom_ops_registered_with_fakes():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    assert hasattr(torch.ops.nerfhip, "siren_fit") and hasattr(torch.ops.nerfhip, "siren_forward")
+    P = SIRENConfig(64, 1, 30.0, "t").num_parameters(64)
+    with FakeTensorMode():
+        t = torch.empty(2, 96, 64)
+        init = torch.empty(2, P)
+        params, losses, rc, rm = torch.ops.nerfhip.siren_fit(t, init, 64, [1, 1], [30.0, 30.0],
+                                                              7, 1e-4)
+        assert params.shape == (2, P) and losses.shape == (2, 7) and rc.shape == (2, 96)
+        y = torch.ops.nerfhip.siren_forward(init[0], torch.empty(96), 64, 1, 30.0, 64)
+        assert y.shape == (96, 64)
