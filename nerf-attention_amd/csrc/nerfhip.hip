@@ -158,7 +158,7 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 // the L2 latency of the weights hides behind ≈2K cycles of MFMA per chunk and
 // the four waves (64 rows) share one copy of every weight.  Per-lane epilogue
 // operands (targets, cos) are issued at the top of the chunk for the same
-// reason.  Rows of the LDS chunk are padded by 16 B so the lanes of one
+// reason.  Rows of the LDS chunk are padded by 32 B so the lanes of one
 // ds_read_b128 (16 rows × 4 k) hit distinct banks.
 // ---------------------------------------------------------------------------
 
@@ -166,12 +166,20 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 // compute, for every 16-row chunk J, acc = src[16J..16J+15][:] · B where the
 // B operand is the register tile b[K/16][4] (lane (c, g) holds B[16kt+4g+s][c]).
 // pre(J) runs at the top of chunk J (issue per-lane loads), epi(J, acc, pre)
-// after its MFMAs.  Ends with a barrier, so `lds` is free afterwards.
-template <int K, int JT, class Pre, class Epi>
+// after its MFMAs (registers only), flush(J) issues chunk J's global stores at
+// the top of chunk J+1, before that chunk's staging loads: vmcnt counts loads
+// and stores together in issue order (MI355X_MICROARCH.md), so a store issued
+// after the staging loads would be waited for at this chunk's barrier; issued
+// before them it has a whole chunk of MFMAs to retire.  Ends with a barrier.
+template <int K, int JT, class Pre, class Epi, class Flush>
 __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float* lds,
                                            const float (&b)[K / 16][4], int tid, int c, int g,
-                                           Pre&& pre, Epi&& epi) {
-  constexpr int LD = K + 4, CH = 16 * LD, NPT = K / 64, C4 = K / 4;
+                                           Pre&& pre, Epi&& epi, Flush&& flush) {
+  // row stride K+8 floats: for the ds_read_b128 lane groups of the A
+  // fragment read (lane (c, g) → dword c·LD + 4g) every start bank is distinct
+  // (a stride of K+4 collides lanes with equal c+g; measured 39 % conflict
+  // cycles).  The staging writes stay contiguous within a row.
+  constexpr int LD = K + 8, CH = 16 * LD, NPT = K / 64, C4 = K / 4;
   f4 st[NPT];
 #pragma unroll
   for (int m = 0; m < NPT; ++m) {
@@ -186,6 +194,7 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
   __syncthreads();
 #pragma unroll
   for (int J = 0; J < JT; ++J) {
+    if (J > 0) flush(J - 1);
     if (J + 1 < JT) {
       const float* nsrc = src + (J + 1) * 16 * K;
 #pragma unroll
@@ -223,6 +232,7 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
     }
     __syncthreads();
   }
+  flush(JT - 1);
 }
 
 // copy n floats (n % 4 == 0, n ≤ 1024) global → LDS, cooperatively
@@ -233,10 +243,9 @@ __device__ __forceinline__ void stage_vec(float* dst, const float* src, int n, i
 // Output width split: a W-wide layer output is produced in NSPLIT passes of
 // W/NSPLIT features; all passes but the last park their fragments in a
 // per-wave LDS stash.  Live output registers drop from W/4 to W/(4·NSPLIT),
-// which is what lets W = 512 fit the 256 VALU-addressable VGPRs and W = 256
-// run two waves per SIMD.
+// which is what lets W = 512 fit the 256 VALU-addressable VGPRs.
 template <int W> struct RowsCfg {
-  static constexpr int NSPLIT = W >= 256 ? 2 : 1;
+  static constexpr int NSPLIT = W >= 512 ? 2 : 1;
   static constexpr int WAVES_PER_SIMD = W >= 512 ? 1 : 2;
 };
 
@@ -244,7 +253,7 @@ template <int W, int D>
 __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_rows(KArgs a) {
   constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
   constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
-  constexpr int WBUF = 2 * 16 * (KMAX + 4);                 // weight double buffer
+  constexpr int WBUF = 2 * 16 * (KMAX + 8);                 // weight double buffer
   constexpr int STASH = (NS - 1) * JP * 256;                // per wave
   __shared__ __attribute__((aligned(16))) float lds[WBUF + KMAX + 4 * STASH];
   float* bias = lds + WBUF;
@@ -282,14 +291,16 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   float ho[JP][4];      // one pass of the layer output
 
   // Run a W-wide output layer as NS passes over src rows; out(Jg, acc, pv)
-  // writes feature tile Jg into ho[Jg % JP]; afterwards hp ← output.
-  auto wide_layer = [&](const float* src, auto& bop, auto&& pre, auto&& out) {
+  // writes feature tile Jg into ho[Jg % JP], flush(Jg) stores it; afterwards
+  // hp ← output.
+  auto wide_layer = [&](const float* src, auto& bop, auto&& pre, auto&& out, auto&& flush) {
 #pragma unroll
     for (int p = 0; p < NS; ++p) {
       gemm_phase<(sizeof(bop) / sizeof(bop[0])) * 16, JP>(
           src + (int64_t)p * JP * 16 * (sizeof(bop) / sizeof(bop[0])) * 16, lds, bop, tid, c,
           g, [&](int J) { return pre(p * JP + J); },
-          [&](int J, f4 acc, f4 pv) { out(p * JP + J, acc, pv); });
+          [&](int J, f4 acc, f4 pv) { out(p * JP + J, acc, pv); },
+          [&](int J) { flush(p * JP + J); });
       if (p + 1 < NS) {
 #pragma unroll
         for (int J = 0; J < JP; ++J) {
@@ -345,23 +356,27 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     stage_vec(bias, Wi + W * W, W, tid);
     float* SHi = SHb + (int64_t)i * WN;
     float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
-    wide_layer(Wi, hp, no_pre, [&](int J, f4 acc, f4) {
-      const f4 bb = ld4(bias + 16 * J + 4 * g);
-      f4 cs;
+    f4 cs_pend;
+    wide_layer(
+        Wi, hp, no_pre,
+        [&](int J, f4 acc, f4) {
+          const f4 bb = ld4(bias + 16 * J + 4 * g);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float z = __fadd_rn(acc[q], bb[q]);
-        float s, co;
-        sincos_fast(__fmul_rn(om, z), &s, &co);
-        ho[J % JP][q] = s;
-        cs[q] = co;
-      }
-      if (train) {
-        st4(SCi + J * 256, cs);
+          for (int q = 0; q < 4; ++q) {
+            const float z = __fadd_rn(acc[q], bb[q]);
+            float s, co;
+            sincos_fast(__fmul_rn(om, z), &s, &co);
+            ho[J % JP][q] = s;
+            cs_pend[q] = co;
+          }
+        },
+        [&](int J) {
+          if (train) {
+            st4(SCi + J * 256, cs_pend);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) SHi[(16 * J + q) * 16] = ho[J % JP][q];
-      }
-    });
+            for (int q = 0; q < 4; ++q) SHi[(16 * J + q) * 16] = ho[J % JP][q];
+          }
+        });
   }
 
   // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f ; MSE ; dL/dŷ
@@ -371,24 +386,28 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + 4 * g : nullptr;
   float y[JD][4];
   float sq = 0.f;
+  f4 y_pend;
   gemm_phase<W, JD>(
       Wf, lds, hp, tid, c, g,
       [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
       [&](int J, f4 acc, f4 t) {
         const f4 bb = ld4(bias + 16 * J + 4 * g);
-        f4 yv;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) yv[q] = __fadd_rn(acc[q], bb[q]);
-        if (yo) st4(yo + 16 * J, yv);             // lane holds ŷ[r][16J+4g+q]
+        for (int q = 0; q < 4; ++q) y_pend[q] = __fadd_rn(acc[q], bb[q]);
         if (train) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float diff = yv[q] - t[q];
+            const float diff = y_pend[q] - t[q];
             sq = valid ? fmaf(diff, diff, sq) : sq;
-            const float gr = valid ? a.grad_scale * diff : 0.f;
-            y[J][q] = gr;
-            SGb[(16 * J + q) * 16] = gr;
+            y[J][q] = valid ? a.grad_scale * diff : 0.f;
           }
+        }
+      },
+      [&](int J) {
+        if (yo) st4(yo + 16 * J, y_pend);          // lane holds ŷ[r][16J+4g+q]
+        if (train) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) SGb[(16 * J + q) * 16] = y[J][q];
         }
       });
   if (!train) return;
@@ -398,24 +417,24 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
 
   // ---- backward.  Each epilogue turns its dH tile into dZ = (dH ⊙ cos(ωz))·ω
   // right away (the next phase's B operand) and stores it for the weight grads.
-  auto dz_out = [&](int layer) {
-    float* SZl = SZb + (int64_t)layer * WN;
-    return [&, SZl](int K, f4 acc, f4 cs) {
+  auto dz_out = [&](int K, f4 acc, f4 cs) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float dz = __fmul_rn(__fmul_rn(acc[q], cs[q]), om);
-        ho[K % JP][q] = dz;
-        SZl[(16 * K + q) * 16] = dz;
-      }
+    for (int q = 0; q < 4; ++q) ho[K % JP][q] = __fmul_rn(__fmul_rn(acc[q], cs[q]), om);
+  };
+  auto dz_store = [&](int layer) {
+    float* SZl = SZb + (int64_t)layer * WN;
+    return [&, SZl](int K) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) SZl[(16 * K + q) * 16] = ho[K % JP][q];
     };
   };
   auto cos_pre = [&](int layer) {
     const float* SCl = SC + (int64_t)layer * WN + (int64_t)rblk * JW * 256 + lane * 4;
     return [SCl](int K) { return ld4(SCl + K * 256); };
   };
-  wide_layer(PT + (int64_t)L * W * W, y, cos_pre(L), dz_out(L));   // W_fᵀ [W][D]
+  wide_layer(PT + (int64_t)L * W * W, y, cos_pre(L), dz_out, dz_store(L));   // W_fᵀ [W][D]
   for (int i = L; i >= 1; --i)
-    wide_layer(PT + (int64_t)(i - 1) * W * W, hp, cos_pre(i - 1), dz_out(i - 1));
+    wide_layer(PT + (int64_t)(i - 1) * W * W, hp, cos_pre(i - 1), dz_out, dz_store(i - 1));
 }
 
 // ---------------------------------------------------------------------------

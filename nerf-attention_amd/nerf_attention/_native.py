@@ -10,6 +10,8 @@ torch's device pointers and streams are valid handles for the engine.
 from __future__ import annotations
 
 import ctypes
+import os
+from pathlib import Path
 from ctypes import c_int32, c_int64, c_void_p, c_char_p, POINTER
 
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
@@ -67,7 +69,8 @@ def load(path=None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB
+    # NERFHIP_LIB: an alternate build of the same ABI (variant A/B on the box)
+    p = path or Path(os.environ.get("NERFHIP_LIB", LIB))
     if not p.exists():
         raise NativeLibraryMissing(
             f"{p} not found: build the HIP engine first "
