@@ -70,6 +70,22 @@ struct KArgs {
   float grad_scale;
 };
 
+#ifdef NERFHIP_STAMPS
+// Diagnostic build only (tools/stamps.py): per-wave s_memtime stamps at the
+// phase boundaries of the row kernel, written to a buffer nothing else reads.
+__device__ unsigned long long* g_stamps = nullptr;
+#define STAMP(k)                                                                       \
+  do {                                                                                 \
+    if (g_stamps && a.mode == 0 && (threadIdx.x & 63) == 0)                            \
+      g_stamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =              \
+          __builtin_amdgcn_s_memtime();                                                \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
@@ -162,77 +178,104 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 // ds_read_b128 (16 rows × 4 k) hit distinct banks.
 // ---------------------------------------------------------------------------
 
+// LDS chunk buffers per GEMM phase: a 3-deep ring where it fits (so the next
+// chunk is already visible while the current one computes), else 2.
+template <int K> constexpr int phase_nbuf() { return K >= 512 ? 2 : 3; }
+template <int K> constexpr int phase_lds_floats() { return phase_nbuf<K>() * 16 * (K + 8); }
+
 // Stream rows [0, 16·JT) of `src` (row-major, row length K) through LDS and
 // compute, for every 16-row chunk J, acc = src[16J..16J+15][:] · B where the
 // B operand is the register tile b[K/16][4] (lane (c, g) holds B[16kt+4g+s][c]).
-// pre(J) runs at the top of chunk J (issue per-lane loads), epi(J, acc, pre)
-// after its MFMAs (registers only), flush(J) issues chunk J's global stores at
-// the top of chunk J+1, before that chunk's staging loads: vmcnt counts loads
-// and stores together in issue order (MI355X_MICROARCH.md), so a store issued
-// after the staging loads would be waited for at this chunk's barrier; issued
-// before them it has a whole chunk of MFMAs to retire.  Ends with a barrier.
-template <int K, int JT, class Pre, class Epi, class Flush>
+//
+// Per chunk J, in issue order:
+//   flush(J−2)        global stores of tile J−2 (two chunks old: vmcnt counts
+//                     loads and stores together in issue order, so stores
+//                     issued after the staging loads would be waited for)
+//   staging loads of chunk J+NBUF−1, pre(J) per-lane loads
+//   K/16 k-steps of 4 MFMAs; A fragments read two steps ahead — across the
+//   chunk boundary when the ring has 3 buffers — and elem(J−1, q, acc, pre)
+//   for q = 0..3 spread over four k-steps: the epilogue VALU (sincos, loss,
+//   dZ) fills MFMA gaps instead of stalling the pipe between chunks
+//   LDS ← staging registers, one barrier.
+// Row stride K+8 floats: every start bank of a ds_read_b128 lane group is
+// distinct (K+4 collides lanes with equal c+g).
+template <int K, int JT, class Pre, class Elem, class Flush>
 __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float* lds,
                                            const float (&b)[K / 16][4], int tid, int c, int g,
-                                           Pre&& pre, Epi&& epi, Flush&& flush) {
-  // row stride K+8 floats: for the ds_read_b128 lane groups of the A
-  // fragment read (lane (c, g) → dword c·LD + 4g) every start bank is distinct
-  // (a stride of K+4 collides lanes with equal c+g; measured 39 % conflict
-  // cycles).  The staging writes stay contiguous within a row.
-  constexpr int LD = K + 8, CH = 16 * LD, NPT = K / 64, C4 = K / 4;
+                                           Pre&& pre, Elem&& elem, Flush&& flush) {
+  constexpr int NB = phase_nbuf<K>();
+  constexpr int LD = K + 8, CH = 16 * LD, NPT = K / 64, C4 = K / 4, KT = K / 16;
+  constexpr int QSTEP = (KT - 1) / 4 > 0 ? (KT - 1) / 4 : 1;
   f4 st[NPT];
+  auto gload = [&](int chunk) {
+    const float* cs = src + chunk * 16 * K;
 #pragma unroll
-  for (int m = 0; m < NPT; ++m) {
-    const int i = tid + 256 * m;
-    st[m] = ld4(src + (i / C4) * K + (i % C4) * 4);
-  }
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + 256 * m;
+      st[m] = ld4(cs + (i / C4) * K + (i % C4) * 4);
+    }
+  };
+  auto lput = [&](int chunk) {
+    float* buf = lds + (chunk % NB) * CH;
 #pragma unroll
-  for (int m = 0; m < NPT; ++m) {
-    const int i = tid + 256 * m;
-    st4(lds + (i / C4) * LD + (i % C4) * 4, st[m]);
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + 256 * m;
+      st4(buf + (i / C4) * LD + (i % C4) * 4, st[m]);
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < NB - 1 && j < JT; ++j) {
+    gload(j);
+    lput(j);
   }
   __syncthreads();
+  const float* lane_off = lds + c * LD + 4 * g;
+  f4 a_cur = ld4(lane_off), a_nxt = ld4(lane_off + 16);
+  f4 acc_prev = {0.f, 0.f, 0.f, 0.f}, pv_prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int J = 0; J < JT; ++J) {
-    if (J > 0) flush(J - 1);
-    if (J + 1 < JT) {
-      const float* nsrc = src + (J + 1) * 16 * K;
-#pragma unroll
-      for (int m = 0; m < NPT; ++m) {
-        const int i = tid + 256 * m;
-        st[m] = ld4(nsrc + (i / C4) * K + (i % C4) * 4);
-      }
-    }
+    if (J >= 2) flush(J - 2);
+    if (J + NB - 1 < JT) gload(J + NB - 1);
     const f4 pv = pre(J);
-    const float* buf = lds + (J & 1) * CH + c * LD + 4 * g;
-    // A fragments read two k-steps ahead; the sched_barrier keeps the
-    // compiler from hoisting every ds_read (and its registers) to the top.
+    const float* buf = lane_off + (J % NB) * CH;
+    const float* nbuf = lane_off + ((J + 1) % NB) * CH;
     f4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    f4 a_cur = ld4(buf), a_nxt = ld4(buf + 16);
 #pragma unroll
-    for (int kt = 0; kt < K / 16; ++kt) {
-      const f4 a_n2 = ld4(buf + 16 * ((kt + 2 < K / 16) ? kt + 2 : kt));
+    for (int kt = 0; kt < KT; ++kt) {
+      f4 a_n2;
+      if (kt + 2 < KT) a_n2 = ld4(buf + 16 * (kt + 2));
+      else if (NB == 3 && J + 1 < JT) a_n2 = ld4(nbuf + 16 * (kt + 2 - KT));
+      else a_n2 = a_nxt;
       f4& ac = acc[kt & 1];
       ac = mfma16(a_cur[0], b[kt][0], ac);
       ac = mfma16(a_cur[1], b[kt][1], ac);
       ac = mfma16(a_cur[2], b[kt][2], ac);
       ac = mfma16(a_cur[3], b[kt][3], ac);
+      if (J > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kq = 1 + q * QSTEP < KT ? 1 + q * QSTEP : KT - 1;
+          if (kt == kq) elem(J - 1, q, acc_prev[q], pv_prev[q]);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
       a_cur = a_nxt;
       a_nxt = a_n2;
     }
-    epi(J, acc[0] + acc[1], pv);
-    if (J + 1 < JT) {
-      float* nbuf = lds + ((J + 1) & 1) * CH;
-#pragma unroll
-      for (int m = 0; m < NPT; ++m) {
-        const int i = tid + 256 * m;
-        st4(nbuf + (i / C4) * LD + (i % C4) * 4, st[m]);
-      }
-    }
+    acc_prev = acc[0] + acc[1];
+    pv_prev = pv;
+    if (J + NB - 1 < JT) lput(J + NB - 1);
     __syncthreads();
+    if (NB == 2 && J + 1 < JT) {  // 2-buffer ring: the next chunk is readable only now
+      a_cur = ld4(nbuf);
+      a_nxt = ld4(nbuf + 16);
+    }
   }
+  if (JT >= 2) flush(JT - 2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) elem(JT - 1, q, acc_prev[q], pv_prev[q]);
   flush(JT - 1);
+  __syncthreads();   // the epilogue read LDS (bias): the next phase may overwrite it
 }
 
 // copy n floats (n % 4 == 0, n ≤ 1024) global → LDS, cooperatively
@@ -253,12 +296,14 @@ template <int W, int D>
 __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_rows(KArgs a) {
   constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
   constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
-  constexpr int WBUF = 2 * 16 * (KMAX + 8);                 // weight double buffer
+  constexpr int WBUF = phase_lds_floats<W>() > phase_lds_floats<D>()
+                           ? phase_lds_floats<W>() : phase_lds_floats<D>();
   constexpr int STASH = (NS - 1) * JP * 256;                // per wave
   __shared__ __attribute__((aligned(16))) float lds[WBUF + KMAX + 4 * STASH];
   float* bias = lds + WBUF;
   int fit, tile;
   if (!map_block(blockIdx.x, a.n_fits, a.n_pad / kRowsPerBlock, fit, tile)) return;
+  STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -290,16 +335,16 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   float hp[JW][4];      // the layer input (B operand), all W features
   float ho[JP][4];      // one pass of the layer output
 
-  // Run a W-wide output layer as NS passes over src rows; out(Jg, acc, pv)
-  // writes feature tile Jg into ho[Jg % JP], flush(Jg) stores it; afterwards
-  // hp ← output.
+  // Run a W-wide output layer as NS passes over src rows; out(Jg, q, acc, pv)
+  // writes element q of feature tile Jg into ho[Jg % JP], flush(Jg) stores
+  // the tile; afterwards hp ← output.
   auto wide_layer = [&](const float* src, auto& bop, auto&& pre, auto&& out, auto&& flush) {
 #pragma unroll
     for (int p = 0; p < NS; ++p) {
       gemm_phase<(sizeof(bop) / sizeof(bop[0])) * 16, JP>(
           src + (int64_t)p * JP * 16 * (sizeof(bop) / sizeof(bop[0])) * 16, lds, bop, tid, c,
           g, [&](int J) { return pre(p * JP + J); },
-          [&](int J, f4 acc, f4 pv) { out(p * JP + J, acc, pv); },
+          [&](int J, int q, float acc, float pv) { out(p * JP + J, q, acc, pv); },
           [&](int J) { flush(p * JP + J); });
       if (p + 1 < NS) {
 #pragma unroll
@@ -350,6 +395,7 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   }
   __syncthreads();
 
+  STAMP(1);
   // ---- hidden SineLayers 1..L: Zᵀ = Wᵢ·Hᵀ (+b), H = sin(ω Z)
   for (int i = 1; i <= L; ++i) {
     const float* Wi = P + off_hidden_w(W, i);
@@ -359,16 +405,12 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     f4 cs_pend;
     wide_layer(
         Wi, hp, no_pre,
-        [&](int J, f4 acc, f4) {
-          const f4 bb = ld4(bias + 16 * J + 4 * g);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float z = __fadd_rn(acc[q], bb[q]);
-            float s, co;
-            sincos_fast(__fmul_rn(om, z), &s, &co);
-            ho[J % JP][q] = s;
-            cs_pend[q] = co;
-          }
+        [&](int J, int q, float acc, float) {
+          const float z = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
+          float s, co;
+          sincos_fast(__fmul_rn(om, z), &s, &co);
+          ho[J % JP][q] = s;
+          cs_pend[q] = co;
         },
         [&](int J) {
           if (train) {
@@ -379,6 +421,7 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
         });
   }
 
+  STAMP(2);
   // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f ; MSE ; dL/dŷ
   const float* Wf = P + off_final_w(W, L);
   stage_vec(bias, Wf + W * D, D, tid);
@@ -390,17 +433,12 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   gemm_phase<W, JD>(
       Wf, lds, hp, tid, c, g,
       [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
-      [&](int J, f4 acc, f4 t) {
-        const f4 bb = ld4(bias + 16 * J + 4 * g);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) y_pend[q] = __fadd_rn(acc[q], bb[q]);
+      [&](int J, int q, float acc, float t) {
+        y_pend[q] = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
         if (train) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float diff = y_pend[q] - t[q];
-            sq = valid ? fmaf(diff, diff, sq) : sq;
-            y[J][q] = valid ? a.grad_scale * diff : 0.f;
-          }
+          const float diff = y_pend[q] - t;
+          sq = valid ? fmaf(diff, diff, sq) : sq;
+          y[J][q] = valid ? a.grad_scale * diff : 0.f;
         }
       },
       [&](int J) {
@@ -410,6 +448,7 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
           for (int q = 0; q < 4; ++q) SGb[(16 * J + q) * 16] = y[J][q];
         }
       });
+  STAMP(3);
   if (!train) return;
   sq = wave_sum(sq);
   if (lane == 0)
@@ -417,9 +456,8 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
 
   // ---- backward.  Each epilogue turns its dH tile into dZ = (dH ⊙ cos(ωz))·ω
   // right away (the next phase's B operand) and stores it for the weight grads.
-  auto dz_out = [&](int K, f4 acc, f4 cs) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) ho[K % JP][q] = __fmul_rn(__fmul_rn(acc[q], cs[q]), om);
+  auto dz_out = [&](int K, int q, float acc, float cs) {
+    ho[K % JP][q] = __fmul_rn(__fmul_rn(acc, cs), om);
   };
   auto dz_store = [&](int layer) {
     float* SZl = SZb + (int64_t)layer * WN;
@@ -433,8 +471,10 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     return [SCl](int K) { return ld4(SCl + K * 256); };
   };
   wide_layer(PT + (int64_t)L * W * W, y, cos_pre(L), dz_out, dz_store(L));   // W_fᵀ [W][D]
+  STAMP(4);
   for (int i = L; i >= 1; --i)
     wide_layer(PT + (int64_t)(i - 1) * W * W, hp, cos_pre(i - 1), dz_out, dz_store(i - 1));
+  STAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -824,6 +864,14 @@ int row_metrics(const KArgs& a, const float* ybuf, int64_t ystride, float* rc, f
 extern "C" {
 
 int nerfhip_abi_version(void) { return NERFHIP_ABI_VERSION; }
+
+#ifdef NERFHIP_STAMPS
+// diagnostic build only: device buffer of [blocks][4 waves][8] u64 stamps
+int nerfhip_debug_set_stamps(unsigned long long* dev_ptr) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess
+             ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+#endif
 
 const char* nerfhip_status_string(int status) {
   switch (status) {

@@ -1,0 +1,56 @@
+"""Per-phase cycle breakdown of k_step_rows from the NERFHIP_STAMPS diagnostic
+build (development tool).  usage:
+    NERFHIP_LIB=build/variants/v_stamps.so python tools/stamps.py --config medium --fits 160
+Stamps (s_memtime, shader clock) per wave: 0 start, 1 after layer 0, 2 after the
+hidden forward, 3 after the final layer, 4 after the backward of the final
+layer, 5 end.  Prints mean cycles per phase next to the wave's MFMA cycles."""
+
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "nerf-attention_amd"))
+
+import numpy as np
+import torch
+
+from nerf_attention import CONFIGS_FULL, CONFIG_WIDE, SIREN, engine, _native
+from nerf_attention.synthetic import kv_slice
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="medium")
+ap.add_argument("--fits", type=int, default=40)
+ap.add_argument("--epochs", type=int, default=3)
+args = ap.parse_args()
+cfgs = {c.name: c for c in CONFIGS_FULL + [CONFIG_WIDE]}
+cfg = cfgs[args.config]
+keys, _ = kv_slice(16, 2, seq_len=2048)
+torch.manual_seed(0)
+specs = [engine.FitSpec(keys, cfg, SIREN(cfg, 128).flat_parameters()) for _ in range(args.fits)]
+job = engine.FitJob(specs, args.epochs, devices=[0])
+g = job.groups[0]
+n_tiles = g.n_pad // 64
+blocks = 8 * n_tiles * ((g.n + 7) // 8)
+buf = torch.zeros(blocks * 4 * 8, dtype=torch.int64, device="cuda")
+lib = _native.load()
+lib.nerfhip_debug_set_stamps.argtypes = [ctypes.c_void_p]
+assert lib.nerfhip_debug_set_stamps(buf.data_ptr()) == 0
+job.launch()
+job.wait()
+st = buf.view(blocks, 4, 8).cpu().numpy().astype(np.float64)
+st = st[st[:, :, 0] > 0]                      # waves that ran (mapped blocks)
+d = np.diff(st[:, :6], axis=1)
+W, L, D = cfg.hidden_features, cfg.hidden_layers, 128
+mf = {"layer0": 0, "hidden_fwd": L * (W // 16) * (W // 16) * 4, "final_fwd": (D // 16) * (W // 16) * 4,
+      "bwd_final": (W // 16) * (D // 16) * 4, "bwd_hidden": L * (W // 16) * (W // 16) * 4}
+out = {}
+for i, name in enumerate(mf):
+    out[name] = {"cycles": round(float(d[:, i].mean())), "mfma": mf[name],
+                 "mfma_cycles_32": mf[name] * 32,
+                 "ratio": round(float(d[:, i].mean()) / max(1, mf[name] * 32), 3)}
+out["total_cycles"] = round(float((st[:, 5] - st[:, 0]).mean()))
+out["waves"] = int(st.shape[0])
+print(json.dumps(out, indent=1))
