@@ -30,6 +30,7 @@
 //   dZ_i   [L_max+1][n_pad/16][W][16]  grad at the pre-activation of layer i
 //   G      [n_pad/16][D][16]           grad at the output (2(ŷ−y)/(N·D))
 //   cos_i  [L_max+1][n_pad/16][W/16][64][4]  cos(ω z), MFMA-fragment order
+//                                      (cos_0 is never stored: recomputed)
 //
 // Numerics: all fp32, inline ≈1-ulp sincos, f32-input MFMA = exact k-ordered
 // fmaf chain.  Parity target: per-fit final cosine within 1e-3 of the
@@ -188,14 +189,17 @@ template <int K> constexpr int phase_lds_floats() { return phase_nbuf<K>() * 16 
 // B operand is the register tile b[K/16][4] (lane (c, g) holds B[16kt+4g+s][c]).
 //
 // Per chunk J, in issue order:
-//   flush(J−2)        global stores of tile J−2 (two chunks old: vmcnt counts
-//                     loads and stores together in issue order, so stores
-//                     issued after the staging loads would be waited for)
+//   flush(J−2)        global stores of tile J−2 (J−1 with a 2-buffer ring): an
+//                     old store, because vmcnt counts loads and stores together
+//                     in issue order, so stores issued after the staging loads
+//                     would be waited for at this chunk's barrier
 //   staging loads of chunk J+NBUF−1, pre(J) per-lane loads
 //   K/16 k-steps of 4 MFMAs; A fragments read two steps ahead — across the
 //   chunk boundary when the ring has 3 buffers — and elem(J−1, q, acc, pre)
 //   for q = 0..3 spread over four k-steps: the epilogue VALU (sincos, loss,
-//   dZ) fills MFMA gaps instead of stalling the pipe between chunks
+//   dZ) fills MFMA gaps instead of stalling the pipe between chunks (3-buffer
+//   ring only; with 2 buffers — one wave per SIMD at K = 512 — elem(J) runs
+//   right after chunk J's MFMAs, which measured faster there)
 //   LDS ← staging registers, one barrier.
 // Row stride K+8 floats: every start bank of a ds_read_b128 lane group is
 // distinct (K+4 collides lanes with equal c+g).
@@ -234,7 +238,11 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
   f4 acc_prev = {0.f, 0.f, 0.f, 0.f}, pv_prev = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int J = 0; J < JT; ++J) {
-    if (J >= 2) flush(J - 2);
+    // pending epilogue results are single-buffered: flush(J') must run before
+    // elem(J'+1), i.e. two chunks late when elem lags a chunk (NB == 3), one
+    // chunk late otherwise
+    if (NB == 3 && J >= 2) flush(J - 2);
+    if (NB == 2 && J >= 1) flush(J - 1);
     if (J + NB - 1 < JT) gload(J + NB - 1);
     const f4 pv = pre(J);
     const float* buf = lane_off + (J % NB) * CH;
@@ -251,7 +259,7 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
       ac = mfma16(a_cur[1], b[kt][1], ac);
       ac = mfma16(a_cur[2], b[kt][2], ac);
       ac = mfma16(a_cur[3], b[kt][3], ac);
-      if (J > 0) {
+      if (NB == 3 && J > 0) {   // (measured: a net loss at one wave/SIMD, NB == 2)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int kq = 1 + q * QSTEP < KT ? 1 + q * QSTEP : KT - 1;
@@ -264,6 +272,10 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
     }
     acc_prev = acc[0] + acc[1];
     pv_prev = pv;
+    if (NB == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) elem(J, q, acc_prev[q], pv_prev[q]);
+    }
     if (J + NB - 1 < JT) lput(J + NB - 1);
     __syncthreads();
     if (NB == 2 && J + 1 < JT) {  // 2-buffer ring: the next chunk is readable only now
@@ -271,9 +283,11 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
       a_nxt = ld4(nbuf + 16);
     }
   }
-  if (JT >= 2) flush(JT - 2);
+  if (NB == 3) {
+    if (JT >= 2) flush(JT - 2);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) elem(JT - 1, q, acc_prev[q], pv_prev[q]);
+    for (int q = 0; q < 4; ++q) elem(JT - 1, q, acc_prev[q], pv_prev[q]);
+  }
   flush(JT - 1);
   __syncthreads();   // the epilogue read LDS (bias): the next phase may overwrite it
 }
@@ -299,15 +313,15 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   constexpr int WBUF = phase_lds_floats<W>() > phase_lds_floats<D>()
                            ? phase_lds_floats<W>() : phase_lds_floats<D>();
   constexpr int STASH = (NS - 1) * JP * 256;                // per wave
-  __shared__ __attribute__((aligned(16))) float lds[WBUF + KMAX + 4 * STASH];
-  float* bias = lds + WBUF;
+  __shared__ __attribute__((aligned(16))) float lds[WBUF + 2 * KMAX + 4 * STASH];
+  float* bias = lds + WBUF;   // a phase's bias, or w0 ‖ b0 in the layer-0 backward
   int fit, tile;
   if (!map_block(blockIdx.x, a.n_fits, a.n_pad / kRowsPerBlock, fit, tile)) return;
   STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
-  float* stash = lds + WBUF + KMAX + wave * STASH + lane * 4;
+  float* stash = lds + WBUF + 2 * KMAX + wave * STASH + lane * 4;
   const int L = a.fit_layers[fit];
   const float om = a.fit_omega[fit];
   const int n_pad = a.n_pad;
@@ -369,28 +383,27 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
       for (int q = 0; q < 4; ++q) hp[(NS - 1) * JP + J][q] = ho[J][q];
   };
 
-  // ---- layer 0: SineLayer(1, W, is_first) — K = 1, an outer product (VALU)
+  // ---- layer 0: SineLayer(1, W, is_first) — K = 1, an outer product (VALU).
+  // cos(ωz0) is not stored: it is a function of (x, w0, b0) and the layer-0
+  // backward recomputes it bit-identically (half this layer's HBM writes).
+  // (Regenerating H0 inside k_step_params as well was measured slower: the
+  // sincos lands on its staging path.)
   stage_vec(lds, P, 2 * W, tid);              // w0 ‖ b0
   __syncthreads();
-  {
-    const float x = a.pos[r];
+  const float x = a.pos[r];
 #pragma unroll
-    for (int J = 0; J < JW; ++J) {
-      const f4 w = ld4(lds + 16 * J + 4 * g), b = ld4(lds + W + 16 * J + 4 * g);
-      f4 cs;
+  for (int J = 0; J < JW; ++J) {
+    const f4 w = ld4(lds + 16 * J + 4 * g), b = ld4(lds + W + 16 * J + 4 * g);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float z = __fadd_rn(__fmul_rn(x, w[q]), b[q]);
-        float s, co;
-        sincos_fast(__fmul_rn(om, z), &s, &co);
-        hp[J][q] = s;
-        cs[q] = co;
-      }
-      if (train) {
-        st4(SC + ((int64_t)rblk * JW + J) * 256 + lane * 4, cs);
+    for (int q = 0; q < 4; ++q) {
+      const float z = __fadd_rn(__fmul_rn(x, w[q]), b[q]);
+      float s, co;
+      sincos_fast(__fmul_rn(om, z), &s, &co);
+      hp[J][q] = s;
+    }
+    if (train) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) SHb[(16 * J + q) * 16] = hp[J][q];
-      }
+      for (int q = 0; q < 4; ++q) SHb[(16 * J + q) * 16] = hp[J][q];
     }
   }
   __syncthreads();
@@ -472,8 +485,19 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   };
   wide_layer(PT + (int64_t)L * W * W, y, cos_pre(L), dz_out, dz_store(L));   // W_fᵀ [W][D]
   STAMP(4);
-  for (int i = L; i >= 1; --i)
+  for (int i = L; i >= 2; --i)
     wide_layer(PT + (int64_t)(i - 1) * W * W, hp, cos_pre(i - 1), dz_out, dz_store(i - 1));
+  // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op sequence
+  stage_vec(bias, P, 2 * W, tid);   // visible after gemm_phase's prologue barrier
+  wide_layer(PT, hp, no_pre,
+             [&](int K, int q, float acc, float) {
+               const int f = 16 * K + 4 * g + q;
+               const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
+               float s, co;
+               sincos_fast(__fmul_rn(om, z), &s, &co);
+               ho[K % JP][q] = __fmul_rn(__fmul_rn(acc, co), om);
+             },
+             dz_store(0));
   STAMP(5);
 }
 
