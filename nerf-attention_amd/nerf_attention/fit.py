@@ -30,20 +30,32 @@ import torch
 
 from . import engine
 from .siren import SIREN, _finish, probe_line
-from .types import CONFIGS_FULL, CONFIGS_QUICK, FitResult, KVMetadata, SIRENConfig
+from .types import CONFIG_WIDE, CONFIGS_FULL, CONFIGS_QUICK, FitResult, KVMetadata, SIRENConfig
 
 
-def select_fits(metadata: KVMetadata, quick: bool):
-    """(layers, heads_per_layer, configs) — reference fit.py:39-48."""
+def select_fits(metadata: KVMetadata, quick: bool, select: str = 'sweep', configs=None):
+    """(layers, heads_per_layer, configs) — reference fit.py:39-48.
+
+    Extensions (default off = reference behaviour): select='all' takes every
+    layer and every KV head (BASELINE config 4's "all layers×heads" scan,
+    SURVEY §3.3); `configs` (names) restricts the architecture list, e.g.
+    ['medium'] or ['wide'] for CONFIG_WIDE."""
     nl = metadata.num_layers
     if quick:
         layers = [0, nl // 2, nl - 1]
-        heads, configs = 1, CONFIGS_QUICK
+        heads, cfgs = 1, CONFIGS_QUICK
     else:
         layers = [0, nl // 4, nl // 2, 3 * nl // 4, nl - 1]
-        heads, configs = min(metadata.num_kv_heads, 4), CONFIGS_FULL
+        heads, cfgs = min(metadata.num_kv_heads, 4), CONFIGS_FULL
+    if select == 'all':
+        layers, heads = list(range(nl)), metadata.num_kv_heads
+    elif select != 'sweep':
+        raise ValueError(f"select must be 'sweep' or 'all', got {select!r}")
+    if configs:
+        known = {c.name: c for c in CONFIGS_FULL + [CONFIG_WIDE]}
+        cfgs = [known[n] for n in configs]
     layers = sorted(set(l for l in layers if l < nl))
-    return layers, heads, configs
+    return layers, heads, cfgs
 
 
 def sweep_plan(layers, heads, configs, load_layer):
@@ -90,9 +102,12 @@ def fit_kv_cache(
     quick: bool = False,
     *,
     gpus: int | None = None,
+    select: str = 'sweep',
+    configs=None,
 ) -> list[dict]:
     """Fit SIRENs to an extracted KV cache and record metrics (fit.py:20-92).
-    `gpus` (extension): farm the fits over this many local GPUs."""
+    Extensions: `gpus` farms the fits over this many local GPUs; `select` and
+    `configs` widen / narrow the selection (see select_fits)."""
     kv_dir, output_dir = Path(kv_dir), Path(output_dir)
     output_dir.mkdir(parents=True, exist_ok=True)
     with open(kv_dir / 'metadata.json') as f:
@@ -105,7 +120,7 @@ def fit_kv_cache(
 
     dev = engine.resolve_device(device)
     devices = [dev.index] if not gpus or gpus <= 1 else list(range(gpus))
-    layers, heads, configs = select_fits(metadata, quick)
+    layers, heads, configs = select_fits(metadata, quick, select, configs)
     total = len(layers) * heads * 2 * len(configs)
 
     def load_layer(layer):
@@ -223,6 +238,10 @@ def main() -> None:
     parser.add_argument('--seed', type=int, default=None,
                         help='torch.manual_seed before the sweep (extension; the reference '
                              'is unseeded)')
+    parser.add_argument('--select', choices=['sweep', 'all'], default='sweep',
+                        help="'all' = every layer x every KV head (extension)")
+    parser.add_argument('--configs', type=str, default=None,
+                        help='comma-separated architecture names, e.g. medium or wide (extension)')
     args = parser.parse_args()
     if args.seed is not None:
         torch.manual_seed(args.seed)
@@ -230,7 +249,8 @@ def main() -> None:
     # this engine has no CPU path, so resolve_device raises instead.
     t0 = time.time()
     fit_kv_cache(Path(args.kv_dir), Path(args.output_dir), args.epochs, args.device,
-                 args.quick, gpus=args.gpus)
+                 args.quick, gpus=args.gpus, select=args.select,
+                 configs=args.configs.split(',') if args.configs else None)
     print(f"\n[nerf-attention-amd] sweep wall clock {time.time() - t0:.2f}s")
 
 

@@ -19,13 +19,16 @@ from .types import KVMetadata
 LLAMA_SHAPE = dict(num_layers=32, num_kv_heads=8, head_dim=128)
 
 
-def sweep_280(seq_len: int = 2048, seed: int | None = 0, quick: bool = False):
+def sweep_280(seq_len: int = 2048, seed: int | None = 0, quick: bool = False,
+              select: str = 'sweep', configs=None):
     """(plan, specs) of the full 280-fit sweep (fit.py:43-47 selection, reference
     record order).  With `seed` set, torch.manual_seed(seed) precedes the inits,
-    which are drawn in the reference's loop order."""
+    which are drawn in the reference's loop order.
+    select='all', configs=['medium'] gives BASELINE config 4's per-seq-len scan
+    (32 layers × 8 heads × K/V = 512 fits)."""
     meta = KVMetadata(model_name='synthetic', seq_len=seq_len, actual_tokens=seq_len,
                       **LLAMA_SHAPE)
-    layers, heads, configs = select_fits(meta, quick)
+    layers, heads, configs = select_fits(meta, quick, select, configs)
 
     def load(layer):
         return kv_layer(layer, seq_len, LLAMA_SHAPE['num_layers'], LLAMA_SHAPE['num_kv_heads'],
