@@ -514,17 +514,22 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
 // ---------------------------------------------------------------------------
 constexpr int kFs = 20;  // LDS floats per feature per 16-row block (16 + pad)
 
-template <int TJ, int TK>
+template <int TJ, int TK, int NW>
 __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict__ A, int FA,
                                         const float* __restrict__ B, int FB, int j0, int k0,
                                         float* P, float* M, float* V, float* PT, int64_t pw,
                                         int64_t pb, int64_t ptw, int out_dim, bool do_bias_tile,
                                         float step_size, float bc2s, float* lds) {
-  constexpr int NA = TJ / 64, NB = TK / 64;            // 32×32 MFMA tiles per wave
-  constexpr int NPT = (TJ + TK) / 64;                  // f4 per thread per block
+  // NW waves as 2 (j) × NW/2 (k); each owns a (TJ/2)×(TK/WK) sub-tile.
+  constexpr int NTH = 64 * NW, WK = NW / 2;
+  constexpr int NA = TJ / 64, NB = TK / WK / 32;       // 32×32 MFMA tiles per wave
+  constexpr int NF4 = (TJ + TK) * 4;                   // f4 per 16-row block
+  constexpr int NPT = (NF4 + NTH - 1) / NTH;           // f4 per thread per block
   constexpr int BUF = (TJ + TK) * kFs;
+  static_assert(NA >= 1 && NB >= 1, "tile too small for the wave grid");
+  static_assert((TJ * 4) % NTH == 0, "A rows must fill whole staging slots");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wj = wave >> 1, wk = wave & 1, h = lane >> 5, lr = lane & 31;
+  const int wj = wave / WK, wk = wave % WK, h = lane >> 5, lr = lane & 31;
   const int n_blocks = a.n_pad / 16;
   const float* Ab = A + (int64_t)j0 * 16;
   const float* Bb = B + (int64_t)k0 * 16;
@@ -533,15 +538,18 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   auto gload = [&](f4 (&st)[NPT], int rb) {
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
-      const int i = tid + 256 * m;
-      st[m] = (i < TJ * 4) ? ld4(Ab + rb * sA + i * 4) : ld4(Bb + rb * sB + (i - TJ * 4) * 4);
+      const int i = tid + NTH * m;      // m < TJ*4/NTH reads A, the rest B: uniform per m
+      if (m < TJ * 4 / NTH)
+        st[m] = ld4(Ab + rb * sA + i * 4);
+      else if (NF4 % NTH == 0 || i < NF4)
+        st[m] = ld4(Bb + rb * sB + (i - TJ * 4) * 4);
     }
   };
   auto lstore = [&](const f4 (&st)[NPT], float* buf) {
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
-      const int i = tid + 256 * m;           // feature i/4, quarter i%4 (A then B)
-      st4(buf + (i >> 2) * kFs + (i & 3) * 4, st[m]);
+      const int i = tid + NTH * m;           // feature i/4, quarter i%4 (A then B)
+      if (NF4 % NTH == 0 || i < NF4) st4(buf + (i >> 2) * kFs + (i & 3) * 4, st[m]);
     }
   };
 
@@ -557,17 +565,20 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   for (int x = 0; x < NA; ++x) bsum[x] = 0.f;
   const bool do_bias = do_bias_tile && wk == 0;
 
+  // n_blocks = n_pad/16 is a multiple of 4.  Prefetches past the end re-read
+  // the last block instead of branching: a conditional load makes the waitcnt
+  // pass assume the worst at the join and drain the fresh prefetch each block.
   f4 st0[NPT], st1[NPT];
   gload(st0, 0);
   lstore(st0, lds);
-  if (n_blocks > 1) gload(st1, 1);
+  gload(st1, 1);
   __syncthreads();
   const float* a_base = lds + (wj * (TJ / 2) + lr) * kFs + 8 * h;
-  const float* b_base = lds + (TJ + wk * (TK / 2) + lr) * kFs + 8 * h;
+  const float* b_base = lds + (TJ + wk * (TK / WK) + lr) * kFs + 8 * h;
 
   auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
     // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
-    if (rb + 2 < n_blocks) gload(st_next, rb + 2);
+    gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
     const int off = (rb & 1) * BUF;
     f4 av[NA][2], bv[NB][2];
 #pragma unroll
@@ -593,21 +604,21 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
         bsum[x] += ((av[x][0][0] + av[x][0][1]) + (av[x][0][2] + av[x][0][3])) +
                    ((av[x][1][0] + av[x][1][1]) + (av[x][1][2] + av[x][1][3]));
     }
-    if (rb + 1 < n_blocks) lstore(st_fill, lds + ((rb + 1) & 1) * BUF);
+    lstore(st_fill, lds + ((rb + 1) & 1) * BUF);   // last block: an unread buffer
     __syncthreads();
   };
   for (int rb = 0; rb < n_blocks; rb += 2) {
     block(rb, st0, st1);
-    if (rb + 1 < n_blocks) block(rb + 1, st1, st0);
+    block(rb + 1, st1, st0);
   }
 
-  // Adam on the wave's (TJ/2)×(TK/2) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
+  // Adam on the wave's (TJ/2)×(TK/WK) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
 #pragma unroll
   for (int x = 0; x < NA; ++x)
 #pragma unroll
     for (int y = 0; y < NB; ++y) {
       const int jrow0 = j0 + wj * (TJ / 2) + 32 * x;
-      const int kcol = k0 + wk * (TK / 2) + 32 * y + lr;
+      const int kcol = k0 + wk * (TK / WK) + 32 * y + lr;
 #pragma unroll
       for (int qb = 0; qb < 4; ++qb) {
         f4 pt;
@@ -639,14 +650,15 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 
 template <int W, int D> struct ParamsCfg {
   static constexpr int T = W < 128 ? W : 128;          // hidden-layer tile (both dims)
+  static constexpr int NW = 4, THREADS = 64 * NW;      // 256-wide tiles measured slower (1 WG/CU)
   static constexpr int TD = D < T ? D : T;             // final-layer tile rows
   static constexpr int NT = W / T;
-  static constexpr int TH = NT * NT, TF = (D / TD) * NT, T0 = W / 64;
+  static constexpr int TH = NT * NT, TF = (D / TD) * NT, T0 = W / (16 * NW);
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
 template <int W, int D>
-__global__ void __launch_bounds__(kThreads, 2) k_step_params(KArgs a) {
+__global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(KArgs a) {
   using C = ParamsCfg<W, D>;
   __shared__ __attribute__((aligned(16))) float lds[2 * (2 * C::T) * kFs];
   int fit, t;
@@ -670,14 +682,14 @@ __global__ void __launch_bounds__(kThreads, 2) k_step_params(KArgs a) {
   if (t < L * C::TH) {
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
-    dw_tile<C::T, C::T>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN, W,
+    dw_tile<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN, W,
                         (u / C::NT) * C::T, (u % C::NT) * C::T, P, M, V, PT, pw,
                         pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
                         (u % C::NT) == 0, step_size, bc2s, lds);
   } else if (t < L * C::TH + C::TF) {
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
-    dw_tile<C::TD, C::T>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
+    dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
                          (u % C::NT) * C::T, P, M, V, PT, pw, pw + (int64_t)W * D,
                          (int64_t)L * W * W, D, (u % C::NT) == 0, step_size, bc2s, lds);
   } else {
@@ -685,7 +697,7 @@ __global__ void __launch_bounds__(kThreads, 2) k_step_params(KArgs a) {
     // f = lane/4 of the wave's 16, quarter m = lane%4 of a 16-row block).
     const int u = t - L * C::TH - C::TF;
     const int f = lane >> 2, m = lane & 3;
-    const int j = u * 64 + wave * 16 + f;
+    const int j = u * (16 * C::NW) + wave * 16 + f;
     const float* zp = SZ + (int64_t)j * 16 + 4 * m;
     const float* xp = a.pos + 4 * m;
     float sw = 0.f, sb = 0.f;
@@ -855,7 +867,8 @@ int launch_rows(const KArgs& a, hipStream_t st) {
 template <int W, int D>
 int launch_params(const KArgs& a, hipStream_t st) {
   const int grid = grid_for(a.n_fits, ParamsCfg<W, D>::tiles(a.L_max));
-  hipLaunchKernelGGL((k_step_params<W, D>), dim3(grid), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL((k_step_params<W, D>), dim3(grid), dim3(ParamsCfg<W, D>::THREADS), 0, st,
+                     a);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
