@@ -136,7 +136,18 @@ __device__ __forceinline__ float wave_sum(float x) {
 // round-robin dispatch, MI355X_MICROARCH.md §Workgroup dispatch); every tile
 // of a fit goes to the same b%8 class so its weights and scratch stay in one
 // XCD's L2.  Speed only — correctness never depends on placement.
+// Groups of fewer than 8 fits map linearly instead: pinning a lone fit to one
+// XCD would leave 7/8 of the chip idle (BASELINE configs 2 and 5).
+constexpr int kXcdMinFits = 8;
+__host__ __device__ inline int grid_for(int n_fits, int n_tiles) {
+  return n_fits < kXcdMinFits ? n_fits * n_tiles : 8 * n_tiles * ((n_fits + 7) / 8);
+}
 __device__ __forceinline__ bool map_block(int b, int n_fits, int n_tiles, int& fit, int& tile) {
+  if (n_fits < kXcdMinFits) {
+    fit = b / n_tiles;
+    tile = b - fit * n_tiles;
+    return true;
+  }
   const int x = b & 7, idx = b >> 3;
   const int slot = idx / n_tiles;
   tile = idx - slot * n_tiles;
@@ -855,7 +866,6 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   return a;
 }
 
-int grid_for(int n_fits, int n_tiles) { return 8 * n_tiles * ((n_fits + 7) / 8); }
 
 template <int W, int D>
 int launch_rows(const KArgs& a, hipStream_t st) {
