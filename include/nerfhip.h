@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NERFHIP_ABI_VERSION 1
+#define NERFHIP_ABI_VERSION 2
 
 typedef enum nerfhip_status {
   NERFHIP_OK = 0,
@@ -57,6 +57,8 @@ typedef struct nerfhip_sizes {
   int64_t stats;           /* D (mean) — std has the same size                */
   int64_t loss_partial;    /* epochs * n_pad/16                               */
   int64_t rows;            /* n_pad (row_cos / row_sq)                        */
+  int64_t grad_split;      /* row splits of the small-group gradient reduction */
+  int64_t grad_partial;    /* grad_split * params: optional split-K workspace  */
 } nerfhip_sizes;
 
 /* One group of fits.  "[n]" = per fit, strided by the matching nerfhip_sizes
@@ -91,6 +93,12 @@ typedef struct nerfhip_group {
   float* row_sq;              /* [n] out: final per-row sum (pred-y)^2 [n_pad] */
   float* probe_row_cos;       /* [n][epochs/log_every][n_pad] or NULL          */
   float* probe_row_sq;        /* [n][epochs/log_every][n_pad] or NULL          */
+  float* grad_partial;        /* [n] optional workspace or NULL.  When set and
+                                 n_fits < 8, each epoch's weight gradient is
+                                 reduced in grad_split row slices (partial
+                                 slabs, then a fixed-order sum + Adam): a small
+                                 group otherwise fills only a few workgroups.
+                                 Deterministic; the split depends on N only.   */
 } nerfhip_group;
 
 int nerfhip_abi_version(void);

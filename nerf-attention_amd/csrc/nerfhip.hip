@@ -69,6 +69,11 @@ struct KArgs {
   float* loss_partial;
   float* y_out;
   float grad_scale;
+  // split-K gradient reduction of small groups (nerfhip.h grad_partial):
+  // n_split row slices write partial slabs gpart[fit][split][param]
+  int32_t n_split;
+  int64_t gp_stride;
+  float* gpart;
 };
 
 #ifdef NERFHIP_STAMPS
@@ -528,6 +533,7 @@ constexpr int kFs = 20;  // LDS floats per feature per 16-row block (16 + pad)
 template <int TJ, int TK, int NW>
 __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict__ A, int FA,
                                         const float* __restrict__ B, int FB, int j0, int k0,
+                                        int rb0, int n_blocks, float* G,
                                         float* P, float* M, float* V, float* PT, int64_t pw,
                                         int64_t pb, int64_t ptw, int out_dim, bool do_bias_tile,
                                         float step_size, float bc2s, float* lds) {
@@ -541,10 +547,11 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   static_assert((TJ * 4) % NTH == 0, "A rows must fill whole staging slots");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wj = wave / WK, wk = wave % WK, h = lane >> 5, lr = lane & 31;
-  const int n_blocks = a.n_pad / 16;
-  const float* Ab = A + (int64_t)j0 * 16;
-  const float* Bb = B + (int64_t)k0 * 16;
+  // rows [16·rb0, 16·(rb0+n_blocks)); G != nullptr: write the partial
+  // gradient there (split-K) instead of applying Adam
   const int64_t sA = (int64_t)FA * 16, sB = (int64_t)FB * 16;
+  const float* Ab = A + (int64_t)j0 * 16 + rb0 * sA;
+  const float* Bb = B + (int64_t)k0 * 16 + rb0 * sB;
 
   auto gload = [&](f4 (&st)[NPT], int rb) {
 #pragma unroll
@@ -576,7 +583,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   for (int x = 0; x < NA; ++x) bsum[x] = 0.f;
   const bool do_bias = do_bias_tile && wk == 0;
 
-  // n_blocks = n_pad/16 is a multiple of 4.  Prefetches past the end re-read
+  // n_blocks is even (nerfhip_group_sizes picks the split).  Prefetches past the end re-read
   // the last block instead of branching: a conditional load makes the waitcnt
   // pass assume the worst at the join and drain the fresh prefetch each block.
   f4 st0[NPT], st1[NPT];
@@ -637,12 +644,16 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
         for (int qq = 0; qq < 4; ++qq) {
           const int j = jrow0 + qq + 8 * qb + 4 * h;
           const int64_t idx = pw + (int64_t)j * a.W + kcol;
+          if (G) {
+            G[idx] = acc[x][y][qb * 4 + qq];
+            continue;
+          }
           float p = P[idx], mm = M[idx], vv = V[idx];
           adam_update(p, mm, vv, acc[x][y][qb * 4 + qq], step_size, bc2s);
           P[idx] = p; M[idx] = mm; V[idx] = vv;
           pt[qq] = p;
         }
-        st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
+        if (!G) st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
       }
     }
   if (do_bias) {
@@ -651,6 +662,10 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
       const float s = bsum[x] + __shfl_xor(bsum[x], 32, 64);
       if (h == 0) {
         const int64_t idx = pb + j0 + wj * (TJ / 2) + 32 * x + lr;
+        if (G) {
+          G[idx] = s;
+          continue;
+        }
         float p = P[idx], mm = M[idx], vv = V[idx];
         adam_update(p, mm, vv, s, step_size, bc2s);
         P[idx] = p; M[idx] = mm; V[idx] = vv;
@@ -673,9 +688,14 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
   using C = ParamsCfg<W, D>;
   __shared__ __attribute__((aligned(16))) float lds[2 * (2 * C::T) * kFs];
   int fit, t;
-  if (!map_block(blockIdx.x, a.n_fits, C::tiles(a.L_max), fit, t)) return;
+  const int nt = C::tiles(a.L_max);
+  if (!map_block(blockIdx.x, a.n_fits, nt * a.n_split, fit, t)) return;
+  const int split = t / nt;
+  t -= split * nt;
   const int L = a.fit_layers[fit];
   if (t >= C::tiles(L)) return;
+  const int nb = a.n_pad / 16 / a.n_split, rb0 = split * nb;
+  float* G = a.n_split > 1 ? a.gpart + fit * a.gp_stride + split * a.p_stride : nullptr;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n_pad = a.n_pad;
   const float step_size = a.sched[2 * a.epoch], bc2s = a.sched[2 * a.epoch + 1];
@@ -694,14 +714,14 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
     dw_tile<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN, W,
-                        (u / C::NT) * C::T, (u % C::NT) * C::T, P, M, V, PT, pw,
+                        (u / C::NT) * C::T, (u % C::NT) * C::T, rb0, nb, G, P, M, V, PT, pw,
                         pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
                         (u % C::NT) == 0, step_size, bc2s, lds);
   } else if (t < L * C::TH + C::TF) {
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
     dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
-                         (u % C::NT) * C::T, P, M, V, PT, pw, pw + (int64_t)W * D,
+                         (u % C::NT) * C::T, rb0, nb, G, P, M, V, PT, pw, pw + (int64_t)W * D,
                          (int64_t)L * W * W, D, (u % C::NT) == 0, step_size, bc2s, lds);
   } else {
     // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0.  Lane = (feature
@@ -713,7 +733,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
     const float* xp = a.pos + 4 * m;
     float sw = 0.f, sb = 0.f;
 #pragma unroll 4
-    for (int rb = 0; rb < n_pad / 16; ++rb) {
+    for (int rb = rb0; rb < rb0 + nb; ++rb) {
       const f4 z = ld4(zp + (int64_t)rb * W * 16), x = ld4(xp + rb * 16);
       sw += (z[0] * x[0] + z[1] * x[1]) + (z[2] * x[2] + z[3] * x[3]);
       sb += (z[0] + z[1]) + (z[2] + z[3]);
@@ -722,7 +742,10 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
     sw += __shfl_xor(sw, 2, 64);
     sb += __shfl_xor(sb, 1, 64);
     sb += __shfl_xor(sb, 2, 64);
-    if (m == 0) {
+    if (m == 0 && G) {
+      G[j] = sw;
+      G[W + j] = sb;
+    } else if (m == 0) {
       float p = P[j], mm = M[j], vv = V[j];
       adam_update(p, mm, vv, sw, step_size, bc2s);
       P[j] = p; M[j] = mm; V[j] = vv;
@@ -730,6 +753,36 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
       adam_update(p, mm, vv, sb, step_size, bc2s);
       P[W + j] = p; M[W + j] = mm; V[W + j] = vv;
     }
+  }
+}
+
+// Split-K second pass: g = Σ_split gpart[split][i] in split order (fixed, so
+// deterministic), then Adam on parameter i and, for weights, the transposed
+// copy.  One thread per canonical parameter index; grid (ceil(P/256), n_fits).
+__global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
+  const int fit = blockIdx.y;
+  const int L = a.fit_layers[fit];
+  const int W = a.W, D = a.D;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_params(W, D, L)) return;
+  const float* g = a.gpart + fit * a.gp_stride + i;
+  float gs = g[0];
+  for (int sp = 1; sp < a.n_split; ++sp) gs += g[sp * a.p_stride];
+  float* P = a.params + fit * a.p_stride;
+  float* M = a.m + fit * a.p_stride;
+  float* V = a.v + fit * a.p_stride;
+  float p = P[i], mm = M[i], vv = V[i];
+  adam_update(p, mm, vv, gs, a.sched[2 * a.epoch], a.sched[2 * a.epoch + 1]);
+  P[i] = p; M[i] = mm; V[i] = vv;
+  float* PT = a.params_t + fit * a.pt_stride;
+  const int64_t fw = off_final_w(W, L);
+  if (i >= fw) {                                       // Wf [D][W] → Wfᵀ [W][D]
+    const int64_t r = i - fw;
+    if (r < (int64_t)D * W) PT[(int64_t)L * W * W + (r % W) * D + r / W] = p;
+  } else if (i >= 2 * W) {                             // Wi [W][W] → Wiᵀ
+    const int64_t r = (i - 2 * W) % ((int64_t)W * W + W);
+    const int64_t layer = (i - 2 * W) / ((int64_t)W * W + W);
+    if (r < (int64_t)W * W) PT[layer * W * W + (r % W) * W + r / W] = p;
   }
 }
 
@@ -848,6 +901,13 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   s->stats = D;
   s->loss_partial = (int64_t)epochs * (n_pad / 16);
   s->rows = n_pad;
+  // split-K row slices for small groups: the largest power of two <= 8 that
+  // leaves every slice an even number (>= 4) of 16-row blocks
+  const int64_t nb = n_pad / 16;
+  int64_t sp = 1;
+  while (sp < 8 && nb % (4 * sp) == 0 && nb / (2 * sp) >= 4) sp *= 2;
+  s->grad_split = sp;
+  s->grad_partial = sp * s->params;
 }
 
 KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
@@ -863,6 +923,9 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   // F.mse_loss backward: grad = (2/numel)·(ŷ−y), the 2/numel a python float
   // rounded to fp32 (TORCH/_decomp/decompositions.py:393-397).
   a.grad_scale = (float)(2.0 / ((double)g->N * (double)g->D));
+  a.n_split = (g->grad_partial && g->n_fits < kXcdMinFits) ? (int32_t)s.grad_split : 1;
+  a.gp_stride = s.grad_partial;
+  a.gpart = g->grad_partial;
   return a;
 }
 
@@ -876,9 +939,13 @@ int launch_rows(const KArgs& a, hipStream_t st) {
 
 template <int W, int D>
 int launch_params(const KArgs& a, hipStream_t st) {
-  const int grid = grid_for(a.n_fits, ParamsCfg<W, D>::tiles(a.L_max));
+  const int grid = grid_for(a.n_fits, ParamsCfg<W, D>::tiles(a.L_max) * a.n_split);
   hipLaunchKernelGGL((k_step_params<W, D>), dim3(grid), dim3(ParamsCfg<W, D>::THREADS), 0, st,
                      a);
+  if (a.n_split > 1) {
+    const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
+    hipLaunchKernelGGL(k_adam_split, dim3(blocks, a.n_fits), dim3(256), 0, st, a);
+  }
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 

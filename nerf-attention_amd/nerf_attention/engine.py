@@ -97,10 +97,13 @@ def resolve_device(device) -> torch.device:
     return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
 
 
+SPLIT_MAX_FITS = 8   # libnerfhip splits the gradient reduction of groups below this size
+
+
 class _Group:
     """Device buffers + descriptor of one (device, W, d, seq_len) group."""
 
-    def __init__(self, members, specs, epochs, lr, log_every, device):
+    def __init__(self, members, specs, epochs, lr, log_every, device, split=True):
         self.members = members
         cfgs = [specs[i].config for i in members]
         t0 = specs[members[0]].target
@@ -153,6 +156,10 @@ class _Group:
         self.eval_y = torch.empty(n, n_pad, self.D, **f32)
         self.row_cos = torch.empty(n, n_pad, **f32)
         self.row_sq = torch.empty(n, n_pad, **f32)
+        # groups of < SPLIT_MAX_FITS fits reduce the weight gradient in row
+        # slices (nerfhip.h grad_partial); the sweep's groups never need it
+        self.grad_partial = torch.empty(n, int(s.grad_partial), **f32) \
+            if split and n < SPLIT_MAX_FITS and s.grad_split > 1 else None
         if self.n_probe:
             self.probe_y = torch.empty(n, self.n_probe, n_pad, self.D, **f32)
             self.probe_row_cos = torch.empty(n, self.n_probe, n_pad, **f32)
@@ -171,7 +178,7 @@ class _Group:
             sched=ptr(self.sched), loss_partial=ptr(self.loss_partial),
             probe_y=ptr(self.probe_y), eval_y=ptr(self.eval_y), row_cos=ptr(self.row_cos),
             row_sq=ptr(self.row_sq), probe_row_cos=ptr(self.probe_row_cos),
-            probe_row_sq=ptr(self.probe_row_sq))
+            probe_row_sq=ptr(self.probe_row_sq), grad_partial=ptr(self.grad_partial))
         with torch.cuda.device(dev):
             self.stream = torch.cuda.Stream(device=dev)
             self.stream.wait_stream(torch.cuda.current_stream(dev))  # H2D copies above
@@ -240,7 +247,7 @@ class FitJob:
     parameters so the same job can be launched again (bench.py's steps)."""
 
     def __init__(self, specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
-                 devices=None):
+                 devices=None, split: bool = True):
         _native.load()
         if devices is None:
             devices = [resolve_device("cuda").index]
@@ -248,7 +255,7 @@ class FitJob:
         self.specs = specs
         self.epochs = epochs
         self.plan = plan_groups(specs, self.devices)
-        self.groups = [_Group(m, specs, epochs, lr, log_every, d) for d, m in self.plan]
+        self.groups = [_Group(m, specs, epochs, lr, log_every, d, split) for d, m in self.plan]
         G = len(self.groups)
         self._descs = (_native.NerfhipGroup * G)(*[g.desc for g in self.groups])
         self._streams = (ctypes.c_void_p * G)(*[g.stream.cuda_stream for g in self.groups])

@@ -58,6 +58,11 @@ def test_group_sizes(lib, W, D, N, L, E):
     assert s.scratch == 3 * (L + 1) * W * n_pad + D * n_pad
     assert s.target == n_pad * D and s.rows == n_pad
     assert s.loss_partial == E * n_pad // 16
+    nb, sp = n_pad // 16, 1           # split-K slices: even, >= 4 blocks each, <= 8
+    while sp < 8 and nb % (4 * sp) == 0 and nb // (2 * sp) >= 4:
+        sp *= 2
+    assert s.grad_split == sp == {2048: 8, 192: 2}[n_pad]
+    assert s.grad_partial == sp * s.params
 
 
 @pytest.mark.parametrize("args,code", [((96, 128, 64, 1, 1), -1), ((64, 96, 64, 1, 1), -2),
