@@ -314,26 +314,66 @@ def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
     return job.outputs()
 
 
+class ForwardPlan:
+    """A SIREN forward bound to device buffers (inference; siren.py:60-61).
+
+    Everything but the kernel launch happens once here: the padded positions,
+    the flat parameter buffer, the per-fit layer/ω tables and the output live
+    on the device, so __call__ is one C-ABI call (nerfhip_siren_forward) on
+    torch's current stream.  `params` may hold several models of the same
+    (config, d_head) as rows [m, P]: one launch evaluates them all, e.g. every
+    K/V head of a layer (the decode-time regeneration the reference profiles,
+    evaluate.py:173-242)."""
+
+    def __init__(self, config: SIRENConfig, d_head: int, positions: torch.Tensor,
+                 n_models: int = 1, device=None):
+        dev = resolve_device(device if device is not None else positions.device)
+        self.config, self.d_head, self.device = config, d_head, dev
+        self.n = int(positions.numel())
+        self.n_models = n_models
+        s = _native.group_sizes(config.hidden_features, d_head, self.n, config.hidden_layers, 0)
+        self.n_pad = int(s.n_pad)
+        self.P = config.num_parameters(d_head)
+        self.pos = torch.zeros(self.n_pad, dtype=torch.float32, device=dev)
+        self.pos[:self.n] = positions.reshape(-1).to(dev, torch.float32)
+        self.params = torch.zeros(n_models, int(s.params), dtype=torch.float32, device=dev)
+        self.layers = torch.full((n_models,), config.hidden_layers, dtype=torch.int32, device=dev)
+        self.omega = torch.full((n_models,), config.omega_0, dtype=torch.float32, device=dev)
+        self.y = torch.empty(n_models, self.n_pad, d_head, dtype=torch.float32, device=dev)
+        self.desc = _native.NerfhipGroup(
+            W=config.hidden_features, D=d_head, N=self.n, n_fits=n_models,
+            L_max=config.hidden_layers, epochs=0, log_every=0, device=dev.index,
+            fit_layers=self.layers.data_ptr(), fit_omega=self.omega.data_ptr(),
+            positions=self.pos.data_ptr(), params=self.params.data_ptr(),
+            eval_y=self.y.data_ptr())
+        self._lib = _native.load()
+
+    def load(self, params: torch.Tensor) -> "ForwardPlan":
+        """Copy flat state_dict-order parameters ([P] or [n_models, P]) in."""
+        self.params[:, :self.P].copy_(params.detach().reshape(self.n_models, self.P))
+        return self
+
+    def __call__(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Run the forward.  Without `out` the result is a view of the plan's
+        buffer [n_models, n, d_head], overwritten by the next call; `out`
+        (fp32, contiguous, [n_models, n_pad, d_head]) receives it instead."""
+        y = self.y if out is None else out
+        if out is not None and (out.shape != self.y.shape or out.dtype != torch.float32
+                                or not out.is_contiguous() or out.device != self.device):
+            raise ValueError(f"out must be a contiguous fp32 {tuple(self.y.shape)} tensor "
+                             f"on {self.device}")
+        self.desc.eval_y = y.data_ptr()
+        stream = torch.cuda.current_stream(self.device)
+        _native.check(self._lib.nerfhip_siren_forward(ctypes.byref(self.desc),
+                                                      stream.cuda_stream))
+        return y[:, :self.n]
+
+
 def forward(params: torch.Tensor, config: SIRENConfig, d_head: int,
             positions: torch.Tensor) -> torch.Tensor:
-    """SIREN forward on the HIP engine (inference; siren.py:60-61).
+    """One-shot SIREN forward on the HIP engine (inference; siren.py:60-61).
     params: flat fp32 state_dict-order vector on a CUDA device;
-    positions: [n] or [n, 1] on the same device.  Returns [n, d_head]."""
-    dev = params.device
-    n = int(positions.numel())
-    s = _native.group_sizes(config.hidden_features, d_head, n, config.hidden_layers, 0)
-    n_pad = int(s.n_pad)
-    pos = torch.zeros(n_pad, dtype=torch.float32, device=dev)
-    pos[:n] = positions.reshape(-1).to(torch.float32)
-    prm = params.detach().to(torch.float32).contiguous()
-    layers = torch.tensor([config.hidden_layers], dtype=torch.int32, device=dev)
-    omega = torch.tensor([config.omega_0], dtype=torch.float32, device=dev)
-    y = torch.empty(n_pad, d_head, dtype=torch.float32, device=dev)
-    g = _native.NerfhipGroup(W=config.hidden_features, D=d_head, N=n, n_fits=1,
-                             L_max=config.hidden_layers, epochs=0, log_every=0,
-                             device=dev.index, fit_layers=layers.data_ptr(),
-                             fit_omega=omega.data_ptr(), positions=pos.data_ptr(),
-                             params=prm.data_ptr(), eval_y=y.data_ptr())
-    stream = torch.cuda.current_stream(dev)
-    _native.check(_native.load().nerfhip_siren_forward(ctypes.byref(g), stream.cuda_stream))
-    return y[:n]
+    positions: [n] or [n, 1] on the same device.  Returns [n, d_head].
+    For repeated calls build a ForwardPlan once."""
+    plan = ForwardPlan(config, d_head, positions, 1, params.device).load(params)
+    return plan()[0]

@@ -72,9 +72,32 @@ class SIREN(nn.Module):
         # module is plain torch, as a CPU nn.Module must be.
         if x.is_cuda and not (torch.is_grad_enabled() and
                               any(p.requires_grad for p in self.parameters())):
-            return engine.forward(self.flat_parameters(), self.siren_config,
-                                  self.out_features, x).to(x.dtype)
+            return self._native_forward(x)
         return self.network(x)
+
+    def _native_forward(self, x: torch.Tensor) -> torch.Tensor:
+        # The plan (device buffers + C-ABI descriptor) is cached across calls:
+        # rebuilt when the position count or device changes, parameters
+        # reloaded when any is replaced or modified in place (data_ptr /
+        # _version).  Positions are copied in every call (N floats).
+        pkey = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        xkey = (x.numel(), x.device)
+        plan = self.__dict__.get('_fwd_plan')
+        if plan is None or self._fwd_xkey != xkey:
+            plan = engine.ForwardPlan(self.siren_config, self.out_features, x, 1, x.device)
+            self._fwd_plan, self._fwd_xkey, self._fwd_pkey = plan, xkey, None
+        else:
+            plan.pos[:plan.n].copy_(x.reshape(-1))
+        if self._fwd_pkey != pkey:
+            plan.load(self.flat_parameters())
+            self._fwd_pkey = pkey
+        out = torch.empty(plan.y.shape, dtype=torch.float32, device=x.device)
+        return plan(out)[0].to(x.dtype)
+
+    def __getstate__(self):
+        # the cached forward plan holds raw device pointers: never pickle it
+        state = super().__getstate__() if hasattr(super(), '__getstate__') else self.__dict__
+        return {k: v for k, v in state.items() if not k.startswith('_fwd_')}
 
     def flat_parameters(self) -> torch.Tensor:
         """All parameters concatenated in state_dict order (the engine's layout)."""
