@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NERFHIP_ABI_VERSION 2
+#define NERFHIP_ABI_VERSION 3
 
 typedef enum nerfhip_status {
   NERFHIP_OK = 0,
@@ -40,8 +40,21 @@ typedef enum nerfhip_status {
   NERFHIP_ERR_BAD_LAYERS = -3,     /* hidden_layers not in [1, NERFHIP_MAX_LAYERS]  */
   NERFHIP_ERR_BAD_SHAPE = -4,      /* seq_len < 2, n_fits < 1, epochs < 0 ...      */
   NERFHIP_ERR_NULL = -5,           /* a required pointer is NULL                   */
-  NERFHIP_ERR_LAUNCH = -6          /* hipGetLastError() after a launch             */
+  NERFHIP_ERR_LAUNCH = -6,         /* hipGetLastError() after a launch             */
+  NERFHIP_ERR_BAD_PRECISION = -7   /* nerfhip_group.precision not a nerfhip_precision */
 } nerfhip_status;
+
+/* Arithmetic of the GEMMs (everything else is fp32 in both modes).
+ *   FP32    v_mfma_f32_*_f32: an exact k-ordered fp32 fma chain.
+ *   BF16X3  fp32 operands split exactly into three bf16 parts (x = h+m+l);
+ *           six bf16 MFMA products per operand pair (the three dropped terms
+ *           are < 2^-23 of the product: fp32-class accuracy) with fp32
+ *           accumulation — 2.7x the matrix-core rate of FP32.  Needs the
+ *           `wsplit` workspace. */
+typedef enum nerfhip_precision {
+  NERFHIP_PRECISION_FP32 = 0,
+  NERFHIP_PRECISION_BF16X3 = 1
+} nerfhip_precision;
 
 #define NERFHIP_MAX_LAYERS 4
 
@@ -59,6 +72,7 @@ typedef struct nerfhip_sizes {
   int64_t rows;            /* n_pad (row_cos / row_sq)                        */
   int64_t grad_split;      /* row splits of the small-group gradient reduction */
   int64_t grad_partial;    /* grad_split * params: optional split-K workspace  */
+  int64_t wsplit;          /* uint16 elements: 6(L_max W^2 + W D), BF16X3 weight planes */
 } nerfhip_sizes;
 
 /* One group of fits.  "[n]" = per fit, strided by the matching nerfhip_sizes
@@ -72,6 +86,8 @@ typedef struct nerfhip_group {
   int32_t epochs;
   int32_t log_every;       /* probe period (siren.py:107); 0 = no probes       */
   int32_t device;          /* HIP device ordinal the buffers and stream live on */
+  int32_t precision;       /* nerfhip_precision (0 = FP32)                     */
+  int32_t reserved;
 
   const int32_t* fit_layers;  /* [n_fits] hidden_layers per fit              */
   const float* fit_omega;     /* [n_fits] omega_0 per fit                    */
@@ -99,6 +115,10 @@ typedef struct nerfhip_group {
                                  slabs, then a fixed-order sum + Adam): a small
                                  group otherwise fills only a few workgroups.
                                  Deterministic; the split depends on N only.   */
+  void* wsplit;               /* [n] uint16 workspace, BF16X3 only (else NULL):
+                                 every weight as exact bf16 split planes, in
+                                 the forward and the transposed orientation,
+                                 rewritten by each Adam step                 */
 } nerfhip_group;
 
 int nerfhip_abi_version(void);

@@ -44,6 +44,9 @@
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -74,6 +77,11 @@ struct KArgs {
   int32_t n_split;
   int64_t gp_stride;
   float* gpart;
+  // bf16x3 precision (NERFHIP_PRECISION_BF16X3): every MFMA weight operand as
+  // exact 3-way bf16 split planes, forward and transposed (xoff layout)
+  int32_t x3;
+  int64_t ws_stride;
+  uint16_t* wsplit;
 };
 
 #ifdef NERFHIP_STAMPS
@@ -135,6 +143,120 @@ __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
   return x;
+}
+
+// ---------------------------------------------------------------------------
+// bf16x3 precision: fp32 GEMMs on the bf16 matrix cores.
+//
+// x = h + m + l EXACTLY, each part a bf16: h keeps the top 8 significant bits
+// of x (truncation), m the next 8 of the remainder, l the last ≤ 8 — both
+// subtractions are exact in fp32.  A product is taken as
+//   x·y ≈ h·h' + (h·l' + l·h' + m·m' + h·m' + m·h')
+// and the dropped terms m·l', l·m', l·l' are < 2^-23·|x·y|: the class of
+// fp32's own product rounding (2^-24), i.e. fp32 accuracy, not bf16.  The
+// five correction products accumulate in their own fp32 accumulator
+// (smallest first), so the h·h' chain takes as many roundings as an f32 MFMA
+// chain.  Per 32-deep k-slice of a 16×16 tile: six v_mfma_f32_16x16x32_bf16
+// (16 cycles each) instead of eight v_mfma_f32_16x16x4_f32 (32 cycles each).
+// ---------------------------------------------------------------------------
+struct S8 {            // one lane's 8 k-values of an MFMA operand, three planes
+  u4 h, m, l;
+};
+
+__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const uint32_t u = __float_as_uint(x);
+  const float r1 = x - __uint_as_float(u & 0xffff0000u);
+  const uint32_t u1 = __float_as_uint(r1);
+  const float r2 = r1 - __uint_as_float(u1 & 0xffff0000u);
+  h = u;
+  m = u1;
+  l = __float_as_uint(r2);   // ≤ 8 significant bits: its top half is exact
+}
+// low half ← bf16 of a, high half ← bf16 of b (the top 16 bits of each)
+__device__ __forceinline__ uint32_t pk_top(uint32_t a, uint32_t b) {
+  return (a >> 16) | (b & 0xffff0000u);
+}
+__device__ __forceinline__ S8 split8(const float (&x)[8]) {
+  uint32_t h[8], m[8], l[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) split3(x[s], h[s], m[s], l[s]);
+  S8 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o.h[i] = pk_top(h[2 * i], h[2 * i + 1]);
+    o.m[i] = pk_top(m[2 * i], m[2 * i + 1]);
+    o.l[i] = pk_top(l[2 * i], l[2 * i + 1]);
+  }
+  return o;
+}
+// the lane's two accumulator tiles t0, t1 (4 features each) as one k-slice
+__device__ __forceinline__ S8 split_pair(const float (&t0)[4], const float (&t1)[4]) {
+  const float x[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return split8(x);
+}
+
+__device__ __forceinline__ f4 mfma16b(u4 a, u4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f16v mfma32b(u4 a, u4 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma16x3(const S8& a, const S8& b, f4& hi, f4& lo) {
+  lo = mfma16b(a.h, b.l, lo);
+  lo = mfma16b(a.l, b.h, lo);
+  lo = mfma16b(a.m, b.m, lo);
+  lo = mfma16b(a.h, b.m, lo);
+  lo = mfma16b(a.m, b.h, lo);
+  hi = mfma16b(a.h, b.h, hi);
+}
+__device__ __forceinline__ void mfma32x3(const S8& a, const S8& b, f16v& hi, f16v& lo) {
+  lo = mfma32b(a.h, b.l, lo);
+  lo = mfma32b(a.l, b.h, lo);
+  lo = mfma32b(a.m, b.m, lo);
+  lo = mfma32b(a.h, b.m, lo);
+  lo = mfma32b(a.m, b.h, lo);
+  hi = mfma32b(a.h, b.h, hi);
+}
+
+// Split-plane layout of a weight matrix M[R][K] (R % 16 == 0, K % 32 == 0):
+// [R/16][K/KC][3 planes][16 rows][KC] bf16, KC = min(K, 256), so a 16-row ×
+// KC sub-chunk of all three planes is one contiguous run.  Inside every
+// 32-wide k-block feature f sits at kperm(f): the order in which a lane
+// (row c, group g) of the B operand holds accumulator tiles 2t and 2t+1 of
+// the layer before — so a lane's 8 k-values are one 16-B read per plane.
+__host__ __device__ constexpr int kc_of(int K) { return K < 256 ? K : 256; }
+__host__ __device__ inline int kperm(int f) {
+  return 8 * ((f & 15) >> 2) + 4 * (f >> 4) + (f & 3);
+}
+__host__ __device__ inline int64_t xoff(int R, int K, int r, int k, int plane) {
+  const int KC = kc_of(K);
+  return ((((int64_t)(r >> 4) * (K / KC) + k / KC) * 3 + plane) * 16 + (r & 15)) * KC +
+         ((k % KC) & ~31) + kperm(k & 31);
+}
+// per-fit split matrices: forward M_i [out][in] for i = 1..L (hidden) and
+// i = L+1 (final, [D][W]), then the transposed M_iᵀ the backward streams
+__host__ __device__ inline int64_t xs_mat(int W, int D, int L, bool bwd, int i) {
+  const int64_t base = bwd ? 3 * ((int64_t)L * W * W + (int64_t)D * W) : 0;
+  return base + (int64_t)(i - 1) * 3 * W * W;
+}
+__host__ __device__ inline int64_t xs_size(int W, int D, int L) {
+  return 6 * ((int64_t)L * W * W + (int64_t)D * W);
+}
+// weight element M_i[j][k] = p into both split copies (prologue / split-K)
+__device__ __forceinline__ void put_w(uint16_t* XS, int W, int D, int L, int i, int j, int k,
+                                      float p) {
+  const int R = i <= L ? W : D;
+  uint32_t h, m, l;
+  split3(p, h, m, l);
+  const uint32_t part[3] = {h >> 16, m >> 16, l >> 16};
+  const int64_t f = xs_mat(W, D, L, false, i), b = xs_mat(W, D, L, true, i);
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+    XS[f + xoff(R, W, j, k, pl)] = (uint16_t)part[pl];
+    XS[b + xoff(W, R, k, j, pl)] = (uint16_t)part[pl];
+  }
 }
 
 // XCD-aware block → (fit, tile).  Blocks b and b+8 share an XCD (observed
@@ -308,6 +430,119 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
   __syncthreads();   // the epilogue read LDS (bias): the next phase may overwrite it
 }
 
+// bf16x3 form of gemm_phase (same contract, same pre/elem/flush schedule with
+// a 3-deep ring): the weight rows arrive as split planes in the xoff layout,
+// one sub-chunk u = J·NH + hh per (output tile J, k-slice hh of NH = K/KC),
+// and each 32-deep k-step is six bf16 MFMAs against the B operand b[K/32]
+// (split k-slices).  LDS image per buffer: [3 planes][16 rows][KC + 16] bf16;
+// the 16-bf16 row pad makes every 16-lane ds_read_b128 group cover the 16
+// slots of a bank row once (row stride ≡ 2 slots mod 16, g adds 1).
+template <int K> constexpr int x3_lds_halfs() { return 3 * 3 * 16 * (kc_of(K) + 16); }
+
+template <int K, int JT, class Pre, class Elem, class Flush>
+__device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, uint16_t* lds,
+                                              const S8 (&b)[K / 32], int tid, int c, int g,
+                                              Pre&& pre, Elem&& elem, Flush&& flush) {
+  constexpr int KC = kc_of(K), NH = K / KC, U = JT * NH, KT = KC / 32;
+  constexpr int LD = KC + 16, PL = 16 * LD, CH = 3 * PL;
+  constexpr int SLP = 2 * KC, SL = 3 * SLP, NPT = (SL + 255) / 256;   // 16-B slots
+  constexpr int QSTEP = (KT - 1) / 4 > 0 ? (KT - 1) / 4 : 1;
+  u4 st[NPT];
+  auto gload = [&](int u) {
+    const uint16_t* cs = src + (int64_t)u * 48 * KC;
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + 256 * m;
+      if (SL % 256 == 0 || i < SL) st[m] = *reinterpret_cast<const u4*>(cs + 8 * i);
+    }
+  };
+  auto lput = [&](int u) {
+    uint16_t* buf = lds + (u % 3) * CH;
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + 256 * m;
+      if (SL % 256 == 0 || i < SL) {
+        const int p = i / SLP, rem = i - p * SLP;
+        *reinterpret_cast<u4*>(buf + p * PL + (rem / (KC / 8)) * LD + (rem % (KC / 8)) * 8) =
+            st[m];
+      }
+    }
+  };
+  const uint16_t* lane_off = lds + c * LD + 8 * g;
+  auto aread = [&](int u, int kt) {
+    const uint16_t* q = lane_off + (u % 3) * CH + 32 * kt;
+    S8 r;
+    r.h = *reinterpret_cast<const u4*>(q);
+    r.m = *reinterpret_cast<const u4*>(q + PL);
+    r.l = *reinterpret_cast<const u4*>(q + 2 * PL);
+    return r;
+  };
+#pragma unroll
+  for (int j = 0; j < 2 && j < U; ++j) {
+    gload(j);
+    lput(j);
+  }
+  __syncthreads();
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  S8 a_cur = aread(0, 0);
+  f4 acc_prev = zero4, pv_prev = zero4, pv = zero4, hi = zero4, lo = zero4;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int J = u / NH, hh = u % NH;
+    if (hh == 0) {
+      if (J >= 2) flush(J - 2);
+      hi = zero4;
+      lo = zero4;
+    }
+    if (u + 2 < U) gload(u + 2);
+    if (hh == 0) pv = pre(J);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      S8 a_nxt = a_cur;
+      if (kt + 1 < KT) a_nxt = aread(u, kt + 1);
+      else if (u + 1 < U) a_nxt = aread(u + 1, 0);
+      mfma16x3(a_cur, b[hh * KT + kt], hi, lo);
+      if (hh == 0 && J > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kq = 1 + q * QSTEP < KT ? 1 + q * QSTEP : KT - 1;
+          if (kt == kq) elem(J - 1, q, acc_prev[q], pv_prev[q]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      a_cur = a_nxt;
+    }
+    if (hh == NH - 1) {
+      acc_prev = hi + lo;
+      pv_prev = pv;
+    }
+    if (u + 2 < U) lput(u + 2);
+    __syncthreads();
+  }
+  if (JT >= 2) flush(JT - 2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) elem(JT - 1, q, acc_prev[q], pv_prev[q]);
+  flush(JT - 1);
+  __syncthreads();   // the epilogue read LDS (bias): the next phase may overwrite it
+}
+
+// one GEMM phase in the kernel's precision (B: float[K/16][4] or S8[K/32])
+template <bool X3, int K, int JT, class B, class Pre, class Elem, class Flush>
+__device__ __forceinline__ void gemm_any(const void* src, float* lds, const B& b, int tid, int c,
+                                         int g, Pre&& pre, Elem&& elem, Flush&& flush) {
+  if constexpr (X3)
+    gemm_phase_x3<K, JT>(static_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(lds), b,
+                         tid, c, g, pre, elem, flush);
+  else
+    gemm_phase<K, JT>(static_cast<const float*>(src), lds, b, tid, c, g, pre, elem, flush);
+}
+
+template <bool C, class A, class B>
+__device__ __forceinline__ auto& pick_ref(A& a, B& b) {
+  if constexpr (C) return a;
+  else return b;
+}
+
 // copy n floats (n % 4 == 0, n ≤ 1024) global → LDS, cooperatively
 __device__ __forceinline__ void stage_vec(float* dst, const float* src, int n, int tid) {
   if (4 * tid < n) st4(dst + 4 * tid, ld4(src + 4 * tid));
@@ -322,12 +557,13 @@ template <int W> struct RowsCfg {
   static constexpr int WAVES_PER_SIMD = W >= 512 ? 1 : 2;
 };
 
-template <int W, int D>
+template <int W, int D, bool X3>
 __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_rows(KArgs a) {
   constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
   constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
-  constexpr int WBUF = phase_lds_floats<W>() > phase_lds_floats<D>()
-                           ? phase_lds_floats<W>() : phase_lds_floats<D>();
+  constexpr int WBUF_F = phase_lds_floats<W>() > phase_lds_floats<D>()
+                             ? phase_lds_floats<W>() : phase_lds_floats<D>();
+  constexpr int WBUF = X3 ? x3_lds_halfs<KMAX>() / 2 : WBUF_F;   // weight ring, in floats
   constexpr int STASH = (NS - 1) * JP * 256;                // per wave
   __shared__ __attribute__((aligned(16))) float lds[WBUF + 2 * KMAX + 4 * STASH];
   float* bias = lds + WBUF;   // a phase's bias, or w0 ‖ b0 in the layer-0 backward
@@ -362,18 +598,28 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   auto no_pre = [&](int) { return zero4; };
 
-  float hp[JW][4];      // the layer input (B operand), all W features
+  float hp[JW][4];      // fp32: the layer input (B operand), all W features
+  S8 hs[JW / 2];        // bf16x3: the same, as split k-slices
   float ho[JP][4];      // one pass of the layer output
+  auto& hb = pick_ref<X3>(hs, hp);    // the B operand of this precision
+  const uint16_t* XS = X3 ? a.wsplit + fit * a.ws_stride : nullptr;
+  // weight operand of layer i (1..L hidden, L+1 final), forward or transposed
+  auto wsrc = [&](bool bwd, int i) -> const void* {
+    if (X3) return XS + xs_mat(W, D, L, bwd, i);
+    if (bwd) return PT + (int64_t)(i - 1) * W * W;
+    return i <= L ? P + off_hidden_w(W, i) : P + off_final_w(W, L);
+  };
 
   // Run a W-wide output layer as NS passes over src rows; out(Jg, q, acc, pv)
   // writes element q of feature tile Jg into ho[Jg % JP], flush(Jg) stores
-  // the tile; afterwards hp ← output.
-  auto wide_layer = [&](const float* src, auto& bop, auto&& pre, auto&& out, auto&& flush) {
+  // the tile; afterwards hb ← output.
+  auto wide_layer = [&](const void* src, auto& bop, auto&& pre, auto&& out, auto&& flush) {
+    constexpr int K = (sizeof(bop) / sizeof(bop[0])) * (X3 ? 32 : 16);
 #pragma unroll
     for (int p = 0; p < NS; ++p) {
-      gemm_phase<(sizeof(bop) / sizeof(bop[0])) * 16, JP>(
-          src + (int64_t)p * JP * 16 * (sizeof(bop) / sizeof(bop[0])) * 16, lds, bop, tid, c,
-          g, [&](int J) { return pre(p * JP + J); },
+      gemm_any<X3, K, JP>(
+          static_cast<const char*>(src) + (int64_t)p * JP * K * (X3 ? 96 : 64), lds, bop, tid,
+          c, g, [&](int J) { return pre(p * JP + J); },
           [&](int J, int q, float acc, float pv) { out(p * JP + J, q, acc, pv); },
           [&](int J) { flush(p * JP + J); });
       if (p + 1 < NS) {
@@ -384,19 +630,29 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
         }
       }
     }
-    // all passes done (gemm_phase ended with a barrier): assemble hp
+    // all passes done (gemm_phase ended with a barrier): assemble the operand
+    auto tile = [&](int Jg, float (&t)[4]) {
+      if (Jg < (NS - 1) * JP) {
+        const f4 v = ld4(stash + Jg * 256);
 #pragma unroll
-    for (int p = 0; p + 1 < NS; ++p)
+        for (int q = 0; q < 4; ++q) t[q] = v[q];
+      } else {
 #pragma unroll
-      for (int J = 0; J < JP; ++J) {
-        const f4 v = ld4(stash + (p * JP + J) * 256);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) hp[p * JP + J][q] = v[q];
+        for (int q = 0; q < 4; ++q) t[q] = ho[Jg - (NS - 1) * JP][q];
       }
+    };
+    if constexpr (X3) {
 #pragma unroll
-    for (int J = 0; J < JP; ++J)
+      for (int J2 = 0; J2 < JW / 2; ++J2) {
+        float t0[4], t1[4];
+        tile(2 * J2, t0);
+        tile(2 * J2 + 1, t1);
+        hs[J2] = split_pair(t0, t1);
+      }
+    } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) hp[(NS - 1) * JP + J][q] = ho[J][q];
+      for (int Jg = 0; Jg < JW; ++Jg) tile(Jg, hp[Jg]);
+    }
   };
 
   // ---- layer 0: SineLayer(1, W, is_first) — K = 1, an outer product (VALU).
@@ -422,6 +678,10 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
       for (int q = 0; q < 4; ++q) SHb[(16 * J + q) * 16] = hp[J][q];
     }
   }
+  if constexpr (X3) {
+#pragma unroll
+    for (int J2 = 0; J2 < JW / 2; ++J2) hs[J2] = split_pair(hp[2 * J2], hp[2 * J2 + 1]);
+  }
   __syncthreads();
 
   STAMP(1);
@@ -433,7 +693,7 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
     f4 cs_pend;
     wide_layer(
-        Wi, hp, no_pre,
+        wsrc(false, i), hb, no_pre,
         [&](int J, int q, float acc, float) {
           const float z = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
           float s, co;
@@ -457,10 +717,11 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + 4 * g;
   float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + 4 * g : nullptr;
   float y[JD][4];
+  S8 ys[JD / 2];
   float sq = 0.f;
   f4 y_pend;
-  gemm_phase<W, JD>(
-      Wf, lds, hp, tid, c, g,
+  gemm_any<X3, W, JD>(
+      wsrc(false, L + 1), lds, hb, tid, c, g,
       [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
       [&](int J, int q, float acc, float t) {
         y_pend[q] = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
@@ -499,13 +760,18 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     const float* SCl = SC + (int64_t)layer * WN + (int64_t)rblk * JW * 256 + lane * 4;
     return [SCl](int K) { return ld4(SCl + K * 256); };
   };
-  wide_layer(PT + (int64_t)L * W * W, y, cos_pre(L), dz_out, dz_store(L));   // W_fᵀ [W][D]
+  if constexpr (X3) {
+#pragma unroll
+    for (int J2 = 0; J2 < JD / 2; ++J2) ys[J2] = split_pair(y[2 * J2], y[2 * J2 + 1]);
+  }
+  auto& yb = pick_ref<X3>(ys, y);
+  wide_layer(wsrc(true, L + 1), yb, cos_pre(L), dz_out, dz_store(L));   // W_fᵀ [W][D]
   STAMP(4);
   for (int i = L; i >= 2; --i)
-    wide_layer(PT + (int64_t)(i - 1) * W * W, hp, cos_pre(i - 1), dz_out, dz_store(i - 1));
+    wide_layer(wsrc(true, i), hb, cos_pre(i - 1), dz_out, dz_store(i - 1));
   // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op sequence
   stage_vec(bias, P, 2 * W, tid);   // visible after gemm_phase's prologue barrier
-  wide_layer(PT, hp, no_pre,
+  wide_layer(wsrc(true, 1), hb, no_pre,
              [&](int K, int q, float acc, float) {
                const int f = 16 * K + 4 * g + q;
                const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
@@ -674,6 +940,178 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   }
 }
 
+// bf16x3 form of dw_tile.  Each staged f4 (feature i/4, rows 4(i%4)..+3 of a
+// 16-row block) is split once, at the LDS store, into three bf16 planes
+// [3][TJ+TK features][kFx] (48-B feature stride: every ds_read_b128 lane
+// group covers a bank row once); a lane then reads its 8 rows of a feature
+// as one 16-B slice per plane, and each (x, y) sub-tile takes six
+// v_mfma_f32_32x32x16_bf16 per 16-row block (hi and correction accumulators)
+// instead of eight v_mfma_f32_32x32x2_f32.  Bias sums come from the fp32
+// staging registers.  The Adam epilogue writes P/M/V and, instead of the
+// transposed fp32 copy, both split copies of the weights for the row kernel.
+constexpr int kFx = 24;
+
+template <int TJ, int TK, int NW>
+__device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
+                                           const float* __restrict__ B, int FB, int j0, int k0,
+                                           int rb0, int n_blocks, float* G, float* P, float* M,
+                                           float* V, uint16_t* XS, int64_t pw, int64_t pb,
+                                           int64_t xf, int64_t xb, int out_dim,
+                                           bool do_bias_tile, float step_size, float bc2s,
+                                           float* lds_f) {
+  constexpr int NTH = 64 * NW, WK = NW / 2;
+  constexpr int NA = TJ / 64, NB = TK / WK / 32;
+  constexpr int NF4 = (TJ + TK) * 4, NPT = (NF4 + NTH - 1) / NTH, NPA = TJ * 4 / NTH;
+  constexpr int PLX = (TJ + TK) * kFx, BUFX = 3 * PLX;
+  static_assert(NA >= 1 && NB >= 1 && NPA >= 1, "tile too small for the wave grid");
+  uint16_t* lds = reinterpret_cast<uint16_t*>(lds_f);
+  const int W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wj = wave / WK, wk = wave % WK, h = lane >> 5, lr = lane & 31;
+  const int64_t sA = (int64_t)FA * 16, sB = (int64_t)FB * 16;
+  const float* Ab = A + (int64_t)j0 * 16 + rb0 * sA;
+  const float* Bb = B + (int64_t)k0 * 16 + rb0 * sB;
+  float bpart[NPA];
+#pragma unroll
+  for (int m = 0; m < NPA; ++m) bpart[m] = 0.f;
+
+  auto gload = [&](f4 (&st)[NPT], int rb) {
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + NTH * m;
+      if (m < NPA)
+        st[m] = ld4(Ab + rb * sA + i * 4);
+      else if (NF4 % NTH == 0 || i < NF4)
+        st[m] = ld4(Bb + rb * sB + (i - TJ * 4) * 4);
+    }
+  };
+  auto lstore = [&](const f4 (&st)[NPT], uint16_t* buf, bool count) {
+#pragma unroll
+    for (int m = 0; m < NPT; ++m) {
+      const int i = tid + NTH * m;
+      if (NF4 % NTH == 0 || i < NF4) {
+        const f4 v = st[m];
+        uint32_t sh[4], sm[4], sl[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) split3(v[s], sh[s], sm[s], sl[s]);
+        uint16_t* d = buf + (i >> 2) * kFx + (i & 3) * 4;
+        const u2 vh = {pk_top(sh[0], sh[1]), pk_top(sh[2], sh[3])};
+        const u2 vm = {pk_top(sm[0], sm[1]), pk_top(sm[2], sm[3])};
+        const u2 vl = {pk_top(sl[0], sl[1]), pk_top(sl[2], sl[3])};
+        *reinterpret_cast<u2*>(d) = vh;
+        *reinterpret_cast<u2*>(d + PLX) = vm;
+        *reinterpret_cast<u2*>(d + 2 * PLX) = vl;
+        if (m < NPA && count) bpart[m] += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+    }
+  };
+
+  f16v hi[NA][NB], lo[NA][NB];
+#pragma unroll
+  for (int x = 0; x < NA; ++x)
+#pragma unroll
+    for (int y = 0; y < NB; ++y)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        hi[x][y][q] = 0.f;
+        lo[x][y][q] = 0.f;
+      }
+
+  f4 st0[NPT], st1[NPT];
+  gload(st0, 0);
+  lstore(st0, lds, true);
+  gload(st1, 1);
+  __syncthreads();
+  const uint16_t* a_base = lds + (wj * (TJ / 2) + lr) * kFx + 8 * h;
+  const uint16_t* b_base = lds + (TJ + wk * (TK / WK) + lr) * kFx + 8 * h;
+  auto rd = [&](const uint16_t* q) {
+    S8 r;
+    r.h = *reinterpret_cast<const u4*>(q);
+    r.m = *reinterpret_cast<const u4*>(q + PLX);
+    r.l = *reinterpret_cast<const u4*>(q + 2 * PLX);
+    return r;
+  };
+
+  auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
+    // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
+    gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
+    const int off = (rb & 1) * BUFX;
+    S8 av[NA], bv[NB];
+#pragma unroll
+    for (int x = 0; x < NA; ++x) av[x] = rd(a_base + off + x * 32 * kFx);
+#pragma unroll
+    for (int y = 0; y < NB; ++y) bv[y] = rd(b_base + off + y * 32 * kFx);
+#pragma unroll
+    for (int x = 0; x < NA; ++x)
+#pragma unroll
+      for (int y = 0; y < NB; ++y) mfma32x3(av[x], bv[y], hi[x][y], lo[x][y]);
+    lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
+    __syncthreads();
+  };
+  for (int rb = 0; rb < n_blocks; rb += 2) {
+    block(rb, st0, st1);
+    block(rb + 1, st1, st0);
+  }
+
+  // Adam on the wave's (TJ/2)×(TK/WK) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
+#pragma unroll
+  for (int x = 0; x < NA; ++x)
+#pragma unroll
+    for (int y = 0; y < NB; ++y) {
+      const int jrow0 = j0 + wj * (TJ / 2) + 32 * x;
+      const int kcol = k0 + wk * (TK / WK) + 32 * y + lr;
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) {
+        uint32_t th[4], tm[4], tl[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int j = jrow0 + qq + 8 * qb + 4 * h;
+          const int64_t idx = pw + (int64_t)j * W + kcol;
+          const float gsum = hi[x][y][qb * 4 + qq] + lo[x][y][qb * 4 + qq];
+          if (G) {
+            G[idx] = gsum;
+            continue;
+          }
+          float p = P[idx], mm = M[idx], vv = V[idx];
+          adam_update(p, mm, vv, gsum, step_size, bc2s);
+          P[idx] = p; M[idx] = mm; V[idx] = vv;
+          split3(p, th[qq], tm[qq], tl[qq]);
+          // forward copy M[j][kcol] of [out_dim][W]
+          XS[xf + xoff(out_dim, W, j, kcol, 0)] = (uint16_t)(th[qq] >> 16);
+          XS[xf + xoff(out_dim, W, j, kcol, 1)] = (uint16_t)(tm[qq] >> 16);
+          XS[xf + xoff(out_dim, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
+        }
+        if (!G) {   // transposed copy: Mᵀ[kcol][j..j+3] is one 8-B run per plane
+          const int jb = jrow0 + 8 * qb + 4 * h;
+          const u2 vh = {pk_top(th[0], th[1]), pk_top(th[2], th[3])};
+          const u2 vm = {pk_top(tm[0], tm[1]), pk_top(tm[2], tm[3])};
+          const u2 vl = {pk_top(tl[0], tl[1]), pk_top(tl[2], tl[3])};
+          *reinterpret_cast<u2*>(XS + xb + xoff(W, out_dim, kcol, jb, 0)) = vh;
+          *reinterpret_cast<u2*>(XS + xb + xoff(W, out_dim, kcol, jb, 1)) = vm;
+          *reinterpret_cast<u2*>(XS + xb + xoff(W, out_dim, kcol, jb, 2)) = vl;
+        }
+      }
+    }
+  if (do_bias_tile) {
+#pragma unroll
+    for (int m = 0; m < NPA; ++m) {
+      float s = bpart[m];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      if ((tid & 3) == 0) {
+        const int64_t idx = pb + j0 + ((tid + NTH * m) >> 2);
+        if (G) {
+          G[idx] = s;
+        } else {
+          float p = P[idx], mm = M[idx], vv = V[idx];
+          adam_update(p, mm, vv, s, step_size, bc2s);
+          P[idx] = p; M[idx] = mm; V[idx] = vv;
+        }
+      }
+    }
+  }
+}
+
 template <int W, int D> struct ParamsCfg {
   static constexpr int T = W < 128 ? W : 128;          // hidden-layer tile (both dims)
   static constexpr int NW = 4, THREADS = 64 * NW;      // 256-wide tiles measured slower (1 WG/CU)
@@ -683,10 +1121,11 @@ template <int W, int D> struct ParamsCfg {
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
-template <int W, int D>
+template <int W, int D, bool X3>
 __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(KArgs a) {
   using C = ParamsCfg<W, D>;
-  __shared__ __attribute__((aligned(16))) float lds[2 * (2 * C::T) * kFs];
+  constexpr int LDS_F = X3 ? 2 * 3 * (2 * C::T) * kFx / 2 : 2 * (2 * C::T) * kFs;
+  __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   int fit, t;
   const int nt = C::tiles(a.L_max);
   if (!map_block(blockIdx.x, a.n_fits, nt * a.n_split, fit, t)) return;
@@ -710,19 +1149,36 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
   const float* SZ = S + (int64_t)(a.L_max + 1) * WN;
   const float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
 
+  uint16_t* XS = X3 ? a.wsplit + fit * a.ws_stride : nullptr;
   if (t < L * C::TH) {
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
-    dw_tile<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN, W,
-                        (u / C::NT) * C::T, (u % C::NT) * C::T, rb0, nb, G, P, M, V, PT, pw,
-                        pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
-                        (u % C::NT) == 0, step_size, bc2s, lds);
+    if constexpr (X3)
+      dw_tile_x3<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W,
+                                    SH + (int64_t)(layer - 1) * WN, W, (u / C::NT) * C::T,
+                                    (u % C::NT) * C::T, rb0, nb, G, P, M, V, XS, pw,
+                                    pw + (int64_t)W * W, xs_mat(W, D, L, false, layer),
+                                    xs_mat(W, D, L, true, layer), W, (u % C::NT) == 0,
+                                    step_size, bc2s, lds);
+    else
+      dw_tile<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN,
+                                 W, (u / C::NT) * C::T, (u % C::NT) * C::T, rb0, nb, G, P, M, V,
+                                 PT, pw, pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
+                                 (u % C::NT) == 0, step_size, bc2s, lds);
   } else if (t < L * C::TH + C::TF) {
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
-    dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
-                         (u % C::NT) * C::T, rb0, nb, G, P, M, V, PT, pw, pw + (int64_t)W * D,
-                         (int64_t)L * W * W, D, (u % C::NT) == 0, step_size, bc2s, lds);
+    if constexpr (X3)
+      dw_tile_x3<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
+                                     (u % C::NT) * C::T, rb0, nb, G, P, M, V, XS, pw,
+                                     pw + (int64_t)W * D, xs_mat(W, D, L, false, L + 1),
+                                     xs_mat(W, D, L, true, L + 1), D, (u % C::NT) == 0,
+                                     step_size, bc2s, lds);
+    else
+      dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
+                                  (u % C::NT) * C::T, rb0, nb, G, P, M, V, PT, pw,
+                                  pw + (int64_t)W * D, (int64_t)L * W * W, D, (u % C::NT) == 0,
+                                  step_size, bc2s, lds);
   } else {
     // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0.  Lane = (feature
     // f = lane/4 of the wave's 16, quarter m = lane%4 of a 16-row block).
@@ -775,14 +1231,21 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   adam_update(p, mm, vv, gs, a.sched[2 * a.epoch], a.sched[2 * a.epoch + 1]);
   P[i] = p; M[i] = mm; V[i] = vv;
   float* PT = a.params_t + fit * a.pt_stride;
+  uint16_t* XS = a.x3 ? a.wsplit + fit * a.ws_stride : nullptr;
   const int64_t fw = off_final_w(W, L);
   if (i >= fw) {                                       // Wf [D][W] → Wfᵀ [W][D]
     const int64_t r = i - fw;
-    if (r < (int64_t)D * W) PT[(int64_t)L * W * W + (r % W) * D + r / W] = p;
+    if (r < (int64_t)D * W) {
+      if (XS) put_w(XS, W, D, L, L + 1, (int)(r / W), (int)(r % W), p);
+      else PT[(int64_t)L * W * W + (r % W) * D + r / W] = p;
+    }
   } else if (i >= 2 * W) {                             // Wi [W][W] → Wiᵀ
     const int64_t r = (i - 2 * W) % ((int64_t)W * W + W);
     const int64_t layer = (i - 2 * W) / ((int64_t)W * W + W);
-    if (r < (int64_t)W * W) PT[layer * W * W + (r % W) * W + r / W] = p;
+    if (r < (int64_t)W * W) {
+      if (XS) put_w(XS, W, D, L, (int)layer + 1, (int)(r / W), (int)(r % W), p);
+      else PT[layer * W * W + (r % W) * W + r / W] = p;
+    }
   }
 }
 
@@ -816,24 +1279,30 @@ __global__ void k_normalize(KArgs a) {
   }
 }
 
-// params_t ← transposed copies of every hidden weight and of the final weight.
+// params_t ← transposed copies of every hidden weight and of the final weight
+// (fp32 precision); wsplit ← both split copies (bf16x3 precision).
 __global__ void k_transpose_params(KArgs a) {
   const int fit = blockIdx.y;
   const int L = a.fit_layers[fit];
   const int W = a.W, D = a.D;
   const int64_t nh = (int64_t)L * W * W, total = nh + (int64_t)W * D;
   const float* P = a.params + fit * a.p_stride;
-  float* PT = a.params_t + fit * a.pt_stride;
+  float* PT = a.params_t ? a.params_t + fit * a.pt_stride : nullptr;
+  uint16_t* XS = a.x3 ? a.wsplit + fit * a.ws_stride : nullptr;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < nh) {
       const int64_t i = e / ((int64_t)W * W), u = e % ((int64_t)W * W);
       const int64_t k = u / W, j = u % W;  // PT_i[k][j] = W_i[j][k]
-      PT[e] = P[off_hidden_w(W, (int)i + 1) + j * W + k];
+      const float p = P[off_hidden_w(W, (int)i + 1) + j * W + k];
+      if (PT) PT[e] = p;
+      if (XS) put_w(XS, W, D, L, (int)i + 1, (int)j, (int)k, p);
     } else {
       const int64_t u = e - nh;
       const int64_t k = u / D, j = u % D;  // WfT[k][j] = Wf[j][k]
-      PT[e] = P[off_final_w(W, L) + j * W + k];
+      const float p = P[off_final_w(W, L) + j * W + k];
+      if (PT) PT[e] = p;
+      if (XS) put_w(XS, W, D, L, L + 1, (int)j, (int)k, p);
     }
   }
 }
@@ -908,6 +1377,7 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   while (sp < 8 && nb % (4 * sp) == 0 && nb / (2 * sp) >= 4) sp *= 2;
   s->grad_split = sp;
   s->grad_partial = sp * s->params;
+  s->wsplit = xs_size(W, D, L_max);
 }
 
 KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
@@ -926,22 +1396,25 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   a.n_split = (g->grad_partial && g->n_fits < kXcdMinFits) ? (int32_t)s.grad_split : 1;
   a.gp_stride = s.grad_partial;
   a.gpart = g->grad_partial;
+  a.x3 = g->precision == NERFHIP_PRECISION_BF16X3;
+  a.ws_stride = s.wsplit;
+  a.wsplit = static_cast<uint16_t*>(g->wsplit);
   return a;
 }
 
 
-template <int W, int D>
+template <int W, int D, bool X3>
 int launch_rows(const KArgs& a, hipStream_t st) {
   const int grid = grid_for(a.n_fits, a.n_pad / kRowsPerBlock);
-  hipLaunchKernelGGL((k_step_rows<W, D>), dim3(grid), dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL((k_step_rows<W, D, X3>), dim3(grid), dim3(kThreads), 0, st, a);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
-template <int W, int D>
+template <int W, int D, bool X3>
 int launch_params(const KArgs& a, hipStream_t st) {
   const int grid = grid_for(a.n_fits, ParamsCfg<W, D>::tiles(a.L_max) * a.n_split);
-  hipLaunchKernelGGL((k_step_params<W, D>), dim3(grid), dim3(ParamsCfg<W, D>::THREADS), 0, st,
-                     a);
+  hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D>::THREADS), 0,
+                     st, a);
   if (a.n_split > 1) {
     const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
     hipLaunchKernelGGL(k_adam_split, dim3(blocks, a.n_fits), dim3(256), 0, st, a);
@@ -951,19 +1424,25 @@ int launch_params(const KArgs& a, hipStream_t st) {
 
 typedef int (*launch_fn)(const KArgs&, hipStream_t);
 
-template <int W>
+template <int W, bool X3>
 void pick_d(int D, launch_fn* rows, launch_fn* params) {
-  if (D == 64) { *rows = launch_rows<W, 64>; *params = launch_params<W, 64>; }
-  else { *rows = launch_rows<W, 128>; *params = launch_params<W, 128>; }
+  if (D == 64) { *rows = launch_rows<W, 64, X3>; *params = launch_params<W, 64, X3>; }
+  else { *rows = launch_rows<W, 128, X3>; *params = launch_params<W, 128, X3>; }
 }
 
-void pick(int W, int D, launch_fn* rows, launch_fn* params) {
+template <bool X3>
+void pick_w(int W, int D, launch_fn* rows, launch_fn* params) {
   switch (W) {
-    case 64: pick_d<64>(D, rows, params); break;
-    case 128: pick_d<128>(D, rows, params); break;
-    case 256: pick_d<256>(D, rows, params); break;
-    default: pick_d<512>(D, rows, params); break;
+    case 64: pick_d<64, X3>(D, rows, params); break;
+    case 128: pick_d<128, X3>(D, rows, params); break;
+    case 256: pick_d<256, X3>(D, rows, params); break;
+    default: pick_d<512, X3>(D, rows, params); break;
   }
+}
+
+void pick(int W, int D, bool x3, launch_fn* rows, launch_fn* params) {
+  if (x3) pick_w<true>(W, D, rows, params);
+  else pick_w<false>(W, D, rows, params);
 }
 
 int row_metrics(const KArgs& a, const float* ybuf, int64_t ystride, float* rc, float* rs,
@@ -996,6 +1475,7 @@ const char* nerfhip_status_string(int status) {
     case NERFHIP_ERR_BAD_SHAPE: return "bad shape (seq_len >= 2, n_fits >= 1, epochs >= 0)";
     case NERFHIP_ERR_NULL: return "a required device pointer is NULL";
     case NERFHIP_ERR_LAUNCH: return "kernel launch failed";
+    case NERFHIP_ERR_BAD_PRECISION: return "precision must be NERFHIP_PRECISION_FP32 or _BF16X3";
     default: return "unknown nerfhip status";
   }
 }
@@ -1014,8 +1494,11 @@ static int check_group(const nerfhip_group* g, bool train) {
   const int rc = validate(g->W, g->D, g->N, g->L_max, g->epochs);
   if (rc != NERFHIP_OK) return rc;
   if (g->n_fits < 1) return NERFHIP_ERR_BAD_SHAPE;
+  if (g->precision != NERFHIP_PRECISION_FP32 && g->precision != NERFHIP_PRECISION_BF16X3)
+    return NERFHIP_ERR_BAD_PRECISION;
   if (!g->fit_layers || !g->fit_omega || !g->positions || !g->params || !g->eval_y)
     return NERFHIP_ERR_NULL;
+  if (g->precision == NERFHIP_PRECISION_BF16X3 && !g->wsplit) return NERFHIP_ERR_NULL;
   if (train && (!g->target || !g->target_norm || !g->mean || !g->std || !g->params_t ||
                 !g->adam_m || !g->adam_v || !g->scratch || !g->sched || !g->loss_partial ||
                 !g->row_cos || !g->row_sq))
@@ -1097,7 +1580,7 @@ GroupRun make_run(const nerfhip_group* g, void* stream) {
   r.st = (hipStream_t)stream;
   fill_sizes(g->W, g->D, g->N, g->L_max, g->epochs, &r.s);
   r.a = make_args(g, r.s);
-  pick(g->W, g->D, &r.rows, &r.params);
+  pick(g->W, g->D, r.a.x3 != 0, &r.rows, &r.params);
   r.n_probe = g->log_every > 0 ? g->epochs / g->log_every : 0;
   r.probe_stride = (int64_t)r.n_probe * r.s.target;
   return r;
@@ -1189,6 +1672,10 @@ int nerfhip_siren_forward(const nerfhip_group* g, void* stream) {
   r.a.mode = 1;
   r.a.y_out = g->eval_y;
   r.a.y_stride = r.s.target;
+  if (r.a.x3) {   // the split weight copies of the current params
+    hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st, r.a);
+    if (hipGetLastError() != hipSuccess) return NERFHIP_ERR_LAUNCH;
+  }
   rc = r.rows(r.a, r.st);
   if (rc == NERFHIP_OK && g->target && g->mean && g->std && g->row_cos && g->row_sq)
     rc = row_metrics(r.a, g->eval_y, r.s.target, g->row_cos, g->row_sq, r.s.rows, r.st);

@@ -18,7 +18,10 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 from ._build import LIB
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+
+# nerfhip_precision (include/nerfhip.h)
+PRECISIONS = {"fp32": 0, "bf16x3": 1}
 
 
 class NerfhipError(RuntimeError):
@@ -32,14 +35,15 @@ class NativeLibraryMissing(NerfhipError):
 class NerfhipSizes(ctypes.Structure):
     _fields_ = [(name, c_int64) for name in (
         "n_pad", "params", "params_t", "scratch", "target", "stats", "loss_partial", "rows",
-        "grad_split", "grad_partial")]
+        "grad_split", "grad_partial", "wsplit")]
 
 
-_GROUP_INTS = ("W", "D", "N", "n_fits", "L_max", "epochs", "log_every", "device")
+_GROUP_INTS = ("W", "D", "N", "n_fits", "L_max", "epochs", "log_every", "device",
+               "precision", "reserved")
 _GROUP_PTRS = ("fit_layers", "fit_omega", "positions", "target", "target_norm", "mean", "std",
                "params", "params_t", "adam_m", "adam_v", "scratch", "sched", "loss_partial",
                "probe_y", "eval_y", "row_cos", "row_sq", "probe_row_cos", "probe_row_sq",
-               "grad_partial")
+               "grad_partial", "wsplit")
 
 
 class NerfhipGroup(ctypes.Structure):

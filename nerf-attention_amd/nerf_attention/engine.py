@@ -99,12 +99,29 @@ def resolve_device(device) -> torch.device:
 
 SPLIT_MAX_FITS = 8   # libnerfhip splits the gradient reduction of groups below this size
 
+# GEMM arithmetic of the engine (include/nerfhip.h nerfhip_precision):
+#   "fp32"   exact fp32 MFMA (v_mfma_f32_*_f32), the reference's arithmetic;
+#   "bf16x3" fp32 operands split exactly into three bf16 parts, six bf16 MFMA
+#            products per pair, fp32 accumulation: fp32-class accuracy at 2.7x
+#            the matrix-core rate.
+PRECISIONS = tuple(_native.PRECISIONS)
+DEFAULT_PRECISION = "fp32"
+
+
+def check_precision(precision):
+    p = DEFAULT_PRECISION if precision is None else precision
+    if p not in _native.PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
+    return p
+
 
 class _Group:
     """Device buffers + descriptor of one (device, W, d, seq_len) group."""
 
-    def __init__(self, members, specs, epochs, lr, log_every, device, split=True):
+    def __init__(self, members, specs, epochs, lr, log_every, device, split=True,
+                 precision="fp32"):
         self.members = members
+        self.precision = precision
         cfgs = [specs[i].config for i in members]
         t0 = specs[members[0]].target
         self.N, self.D = int(t0.shape[0]), int(t0.shape[1])
@@ -160,6 +177,8 @@ class _Group:
         # slices (nerfhip.h grad_partial); the sweep's groups never need it
         self.grad_partial = torch.empty(n, int(s.grad_partial), **f32) \
             if split and n < SPLIT_MAX_FITS and s.grad_split > 1 else None
+        self.wsplit = torch.empty(n, int(s.wsplit), dtype=torch.int16, device=dev) \
+            if precision == "bf16x3" else None
         if self.n_probe:
             self.probe_y = torch.empty(n, self.n_probe, n_pad, self.D, **f32)
             self.probe_row_cos = torch.empty(n, self.n_probe, n_pad, **f32)
@@ -170,7 +189,7 @@ class _Group:
         ptr = lambda t: None if t is None else t.data_ptr()
         self.desc = _native.NerfhipGroup(
             W=self.W, D=self.D, N=self.N, n_fits=n, L_max=self.L_max, epochs=epochs,
-            log_every=self.log_every, device=device,
+            log_every=self.log_every, device=device, precision=_native.PRECISIONS[precision],
             fit_layers=ptr(self.layers), fit_omega=ptr(self.omega), positions=ptr(self.pos),
             target=ptr(self.target), target_norm=ptr(self.target_norm), mean=ptr(self.mean),
             std=ptr(self.std), params=ptr(self.params), params_t=ptr(self.params_t),
@@ -178,7 +197,8 @@ class _Group:
             sched=ptr(self.sched), loss_partial=ptr(self.loss_partial),
             probe_y=ptr(self.probe_y), eval_y=ptr(self.eval_y), row_cos=ptr(self.row_cos),
             row_sq=ptr(self.row_sq), probe_row_cos=ptr(self.probe_row_cos),
-            probe_row_sq=ptr(self.probe_row_sq), grad_partial=ptr(self.grad_partial))
+            probe_row_sq=ptr(self.probe_row_sq), grad_partial=ptr(self.grad_partial),
+            wsplit=ptr(self.wsplit))
         with torch.cuda.device(dev):
             self.stream = torch.cuda.Stream(device=dev)
             self.stream.wait_stream(torch.cuda.current_stream(dev))  # H2D copies above
@@ -247,15 +267,17 @@ class FitJob:
     parameters so the same job can be launched again (bench.py's steps)."""
 
     def __init__(self, specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
-                 devices=None, split: bool = True):
+                 devices=None, split: bool = True, precision: str | None = None):
         _native.load()
+        self.precision = check_precision(precision)
         if devices is None:
             devices = [resolve_device("cuda").index]
         self.devices = [resolve_device(torch.device("cuda", d)).index for d in devices]
         self.specs = specs
         self.epochs = epochs
         self.plan = plan_groups(specs, self.devices)
-        self.groups = [_Group(m, specs, epochs, lr, log_every, d, split) for d, m in self.plan]
+        self.groups = [_Group(m, specs, epochs, lr, log_every, d, split, self.precision)
+                       for d, m in self.plan]
         G = len(self.groups)
         self._descs = (_native.NerfhipGroup * G)(*[g.desc for g in self.groups])
         self._streams = (ctypes.c_void_p * G)(*[g.stream.cuda_stream for g in self.groups])
@@ -303,12 +325,12 @@ class FitJob:
 
 
 def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
-             devices=None) -> list:
+             devices=None, precision: str | None = None) -> list:
     """Train every FitSpec for `epochs` Adam steps; returns FitOutput per spec
     (same order).  Blocks until the device work is done."""
     if not specs:
         return []
-    job = FitJob(specs, epochs, lr, log_every, devices)
+    job = FitJob(specs, epochs, lr, log_every, devices, precision=precision)
     job.launch()
     job.wait()
     return job.outputs()

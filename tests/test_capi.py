@@ -63,6 +63,7 @@ def test_group_sizes(lib, W, D, N, L, E):
         sp *= 2
     assert s.grad_split == sp == {2048: 8, 192: 2}[n_pad]
     assert s.grad_partial == sp * s.params
+    assert s.wsplit == 6 * (L * W * W + W * D)        # bf16x3 split planes, fwd + transposed
 
 
 @pytest.mark.parametrize("args,code", [((96, 128, 64, 1, 1), -1), ((64, 96, 64, 1, 1), -2),
@@ -82,3 +83,5 @@ def test_fit_rejects_before_touching_device(lib):
     assert lib.nerfhip_siren_fit(None, 1, streams) == -5
     assert lib.nerfhip_siren_fit_timed(ctypes.byref(g), 1, streams, None) == -5
     assert lib.nerfhip_siren_forward(None, None) == -5
+    g.W, g.precision = 256, 7
+    assert lib.nerfhip_siren_fit(ctypes.byref(g), 1, streams) == -7      # unknown precision

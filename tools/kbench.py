@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=50)
     ap.add_argument("--seq-len", type=int, default=2048)
     ap.add_argument("--repeat", type=int, default=2)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"])
     args = ap.parse_args()
     cfgs = {c.name: c for c in CONFIGS_FULL + [CONFIG_WIDE]}
     names = args.config.split(",")
@@ -41,7 +42,7 @@ def main():
         cfg = cfgs[names[i % len(names)]]
         specs.append(engine.FitSpec(keys if i % 2 == 0 else vals, cfg,
                                     SIREN(cfg, 128).flat_parameters()))
-    job = engine.FitJob(specs, args.epochs, devices=[0])
+    job = engine.FitJob(specs, args.epochs, devices=[0], precision=args.precision)
     assert len(job.groups) == 1, "kbench times one group: use configs of one width"
     g = job.groups[0]
     cf = [specs[i].config for i in g.members]
@@ -52,7 +53,7 @@ def main():
         t = job.timing[0]
         rows_ms, par_ms = t.rows_ms / t.launches, t.params_ms / t.launches
         fr, fp = rows_flops(args.seq_len, 128, cf), params_flops(args.seq_len, 128, cf)
-        out.append({"rep": rep, "config": args.config, "fits": g.n, "W": g.W,
+        out.append({"rep": rep, "config": args.config, "precision": args.precision, "fits": g.n, "W": g.W,
                     "rows_ms": round(rows_ms, 4), "params_ms": round(par_ms, 4),
                     "rows_tflops": round(fr / rows_ms / 1e9, 2),
                     "params_tflops": round(fp / par_ms / 1e9, 2),
