@@ -93,6 +93,7 @@ def main() -> None:
     ap.add_argument("--cpu-sample-epochs", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,7 +110,8 @@ def main() -> None:
     n_total = len(specs)
     costs = [engine.fit_flops(args.seq_len, 128, s.config, args.epochs) for s in specs]
     mine = farm.rank_share(costs, world, rank)
-    job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[local])
+    job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[local],
+                        precision=args.precision)
 
     for _ in range(args.warmup):
         job.launch()

@@ -24,13 +24,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="medium")
 ap.add_argument("--fits", type=int, default=40)
 ap.add_argument("--epochs", type=int, default=3)
+ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"])
 args = ap.parse_args()
 cfgs = {c.name: c for c in CONFIGS_FULL + [CONFIG_WIDE]}
 cfg = cfgs[args.config]
 keys, _ = kv_slice(16, 2, seq_len=2048)
 torch.manual_seed(0)
 specs = [engine.FitSpec(keys, cfg, SIREN(cfg, 128).flat_parameters()) for _ in range(args.fits)]
-job = engine.FitJob(specs, args.epochs, devices=[0])
+job = engine.FitJob(specs, args.epochs, devices=[0], precision=args.precision)
 g = job.groups[0]
 n_tiles = g.n_pad // 64
 blocks = 8 * n_tiles * ((g.n + 7) // 8)
@@ -46,11 +47,14 @@ d = np.diff(st[:, :6], axis=1)
 W, L, D = cfg.hidden_features, cfg.hidden_layers, 128
 mf = {"layer0": 0, "hidden_fwd": L * (W // 16) * (W // 16) * 4, "final_fwd": (D // 16) * (W // 16) * 4,
       "bwd_final": (W // 16) * (D // 16) * 4, "bwd_hidden": L * (W // 16) * (W // 16) * 4}
-out = {}
+# MFMA pipe cycles per wave: f32 16x16x4 = 32 cycles each; bf16x3 = 6 x 16x16x32
+# (16 cycles) per 8 f32 16x16x4 = 12 cycles per f32-MFMA equivalent
+cyc = 32 if args.precision == "fp32" else 12
+out = {"precision": args.precision}
 for i, name in enumerate(mf):
-    out[name] = {"cycles": round(float(d[:, i].mean())), "mfma": mf[name],
-                 "mfma_cycles_32": mf[name] * 32,
-                 "ratio": round(float(d[:, i].mean()) / max(1, mf[name] * 32), 3)}
+    out[name] = {"cycles": round(float(d[:, i].mean())), "mfma_f32_equiv": mf[name],
+                 "mfma_pipe_cycles": mf[name] * cyc,
+                 "ratio": round(float(d[:, i].mean()) / max(1, mf[name] * cyc), 3)}
 out["total_cycles"] = round(float((st[:, 5] - st[:, 0]).mean()))
 out["waves"] = int(st.shape[0])
 print(json.dumps(out, indent=1))
