@@ -62,7 +62,7 @@ typedef enum nerfhip_precision {
  * needs.  Filled by nerfhip_group_sizes(); the caller allocates
  * n_fits * <per-fit size> for the per-fit buffers. */
 typedef struct nerfhip_sizes {
-  int64_t n_pad;           /* seq_len rounded up to the 64-row tile           */
+  int64_t n_pad;           /* seq_len rounded up to 64 rows (row workgroups)  */
   int64_t params;          /* P(L_max) = 2W + L(W^2+W) + W*D + D  (state_dict order) */
   int64_t params_t;        /* transposed weight copies: L_max*W^2 + W*D       */
   int64_t scratch;         /* activations / grads / cos, feature-major        */

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <type_traits>
 
 #include "nerfhip.h"
 
@@ -50,8 +51,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-constexpr int kRowsPerBlock = 64;   // 4 waves × 16 rows
-constexpr int kThreads = 256;
+constexpr int kRowPad = 64;    // n_pad granule: a whole number of row workgroups
 
 struct KArgs {
   int32_t W, D, N, n_pad, n_fits, L_max, epochs, epoch, mode;
@@ -91,13 +91,24 @@ __device__ unsigned long long* g_stamps = nullptr;
 #define STAMP(k)                                                                       \
   do {                                                                                 \
     if (g_stamps && a.mode == 0 && (threadIdx.x & 63) == 0)                            \
-      g_stamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =              \
+      g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = \
           __builtin_amdgcn_s_memtime();                                                \
   } while (0)
+// accumulate cycles into stamp slot k (8..15) of this wave
+#define STAMP_ADD(k, v)                                                                \
+  do {                                                                                 \
+    if (g_stamps && (threadIdx.x & 63) == 0)                                           \
+      g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] += (v); \
+  } while (0)
+#define MEMTIME() __builtin_amdgcn_s_memtime()
 #else
 #define STAMP(k) \
   do {           \
   } while (0)
+#define STAMP_ADD(k, v) \
+  do {                  \
+  } while (0)
+#define MEMTIME() 0ull
 #endif
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
@@ -341,28 +352,29 @@ template <int K> constexpr int phase_lds_floats() { return phase_nbuf<K>() * 16 
 //   LDS ← staging registers, one barrier.
 // Row stride K+8 floats: every start bank of a ds_read_b128 lane group is
 // distinct (K+4 collides lanes with equal c+g).
-template <int K, int JT, class Pre, class Elem, class Flush>
+template <int K, int JT, int NTH, class Pre, class Elem, class Flush>
 __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float* lds,
                                            const float (&b)[K / 16][4], int tid, int c, int g,
                                            Pre&& pre, Elem&& elem, Flush&& flush) {
   constexpr int NB = phase_nbuf<K>();
-  constexpr int LD = K + 8, CH = 16 * LD, NPT = K / 64, C4 = K / 4, KT = K / 16;
+  constexpr int LD = K + 8, CH = 16 * LD, C4 = K / 4, KT = K / 16;
+  constexpr int NF4 = 16 * C4, NPT = (NF4 + NTH - 1) / NTH;   // f4 slots per chunk
   constexpr int QSTEP = (KT - 1) / 4 > 0 ? (KT - 1) / 4 : 1;
   f4 st[NPT];
   auto gload = [&](int chunk) {
     const float* cs = src + chunk * 16 * K;
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
-      const int i = tid + 256 * m;
-      st[m] = ld4(cs + (i / C4) * K + (i % C4) * 4);
+      const int i = tid + NTH * m;
+      if (NF4 % NTH == 0 || i < NF4) st[m] = ld4(cs + (i / C4) * K + (i % C4) * 4);
     }
   };
   auto lput = [&](int chunk) {
     float* buf = lds + (chunk % NB) * CH;
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
-      const int i = tid + 256 * m;
-      st4(buf + (i / C4) * LD + (i % C4) * 4, st[m]);
+      const int i = tid + NTH * m;
+      if (NF4 % NTH == 0 || i < NF4) st4(buf + (i / C4) * LD + (i % C4) * 4, st[m]);
     }
   };
 #pragma unroll
@@ -430,95 +442,183 @@ __device__ __forceinline__ void gemm_phase(const float* __restrict__ src, float*
   __syncthreads();   // the epilogue read LDS (bias): the next phase may overwrite it
 }
 
-// bf16x3 form of gemm_phase (same contract, same pre/elem/flush schedule with
-// a 3-deep ring): the weight rows arrive as split planes in the xoff layout,
-// one sub-chunk u = J·NH + hh per (output tile J, k-slice hh of NH = K/KC),
-// and each 32-deep k-step is six bf16 MFMAs against the B operand b[K/32]
-// (split k-slices).  LDS image per buffer: [3 planes][16 rows][KC + 16] bf16;
-// the 16-bf16 row pad makes every 16-lane ds_read_b128 group cover the 16
-// slots of a bank row once (row stride ≡ 2 slots mod 16, g adds 1).
-template <int K> constexpr int x3_lds_halfs() { return 3 * 3 * 16 * (kc_of(K) + 16); }
+// bf16x3 form of gemm_phase (same contract, same pre/elem/flush schedule):
+// the weight rows arrive as split planes in the xoff layout, one sub-chunk
+// u = J·NH + hh per (output tile J, k-slice hh of NH = K/KC), and each 32-deep
+// k-step is six bf16 MFMAs against the B operand b[K/32] (split k-slices).
+//
+// Staging is LDS-DMA (global_load_lds_dwordx4) into a 3-deep ring of its own
+// __shared__ object: sub-chunk u+2 is issued at the top of sub-chunk u and
+// only retired (counted vmcnt, then the barrier) at the END of u+1, so every
+// fill has two sub-chunks of MFMA time to land and costs no VGPRs.  The DMA
+// image is lane-linear, so the bank swizzle lives on the source address:
+// 16-B slot s of row r sits at physical slot s ^ (r mod min(16, slots/row)),
+// which makes every 16-lane ds_read_b128 group of the A-fragment read hit the
+// 16 slots of a bank row once.  The A fragments are read by inline-asm
+// ds_read_b128 (hipcc would otherwise put a vmcnt(0) drain of the in-flight
+// DMA in front of them) and retired by an lgkmcnt wait that also redefines
+// the fragment registers, so no use can be scheduled before the data lands.
+template <int K> constexpr int x3_ring_halfs() { return 3 * 3 * 16 * kc_of(K); }
 
-template <int K, int JT, class Pre, class Elem, class Flush>
-__device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, uint16_t* lds,
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int N> constexpr std::integral_constant<int, N> ic{};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// ds_read_b128 at base + OFF bytes; OFF must fit the 16-bit offset field
+template <int OFF>
+__device__ __forceinline__ u4 ds_read16(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  u4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+
+template <int K, int JT, int NTH, int NST, int NLD, class Pre, class Elem, class Flush>
+__device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, uint16_t* ring,
                                               const S8 (&b)[K / 32], int tid, int c, int g,
                                               Pre&& pre, Elem&& elem, Flush&& flush) {
   constexpr int KC = kc_of(K), NH = K / KC, U = JT * NH, KT = KC / 32;
-  constexpr int LD = KC + 16, PL = 16 * LD, CH = 3 * PL;
-  constexpr int SLP = 2 * KC, SL = 3 * SLP, NPT = (SL + 255) / 256;   // 16-B slots
+  constexpr int SR = KC / 8;                                // 16-B slots per row
+  constexpr int SWM = (SR < 16 ? SR : 16) - 1;              // swizzle mask
+  constexpr int CH = 3 * 16 * KC;                           // bf16 per ring buffer
+  constexpr int PLB = 32 * KC;                              // bytes per plane
+  constexpr int SL = 3 * 16 * SR, NPT = (SL + NTH - 1) / NTH;   // slots per sub-chunk
+  constexpr int NDMA = SL / NTH;                                // DMAs every wave issues
   constexpr int QSTEP = (KT - 1) / 4 > 0 ? (KT - 1) / 4 : 1;
-  u4 st[NPT];
-  auto gload = [&](int u) {
-    const uint16_t* cs = src + (int64_t)u * 48 * KC;
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int wave = tid >> 6;
+  // this lane's source offset (bf16) inside a sub-chunk, per DMA round
+  int soff[NPT];
 #pragma unroll
-    for (int m = 0; m < NPT; ++m) {
-      const int i = tid + 256 * m;
-      if (SL % 256 == 0 || i < SL) st[m] = *reinterpret_cast<const u4*>(cs + 8 * i);
-    }
+  for (int m = 0; m < NPT; ++m) {
+    const int i = tid + NTH * m;
+    const int row = (i / SR) & 15, pl = i / (16 * SR), ps = i % SR;
+    soff[m] = (pl * 16 + row) * KC + 8 * (ps ^ (row & SWM));
+  }
+  // buffer-resource form: SGPR base + per-lane 32-bit offset + SGPR sub-chunk offset
+  // (a flat-pointer global_load_lds makes hipcc materialise a 64-bit address per
+  // sub-chunk and round)
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000);
+  auto dma_round = [&](int u, int m) {
+    uint16_t* buf = ring + (u % 3) * CH;
+    if (SL % NTH == 0 || NTH * m + 64 * wave < SL)   // wave-uniform
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (lds_void*)(buf + 8 * (NTH * m + 64 * wave)), 16, 2 * soff[m], u * 96 * KC, 0,
+          0);
   };
-  auto lput = [&](int u) {
-    uint16_t* buf = lds + (u % 3) * CH;
+  auto dma = [&](int u) {
 #pragma unroll
-    for (int m = 0; m < NPT; ++m) {
-      const int i = tid + 256 * m;
-      if (SL % 256 == 0 || i < SL) {
-        const int p = i / SLP, rem = i - p * SLP;
-        *reinterpret_cast<u4*>(buf + p * PL + (rem / (KC / 8)) * LD + (rem % (KC / 8)) * 8) =
-            st[m];
-      }
-    }
+    for (int m = 0; m < NPT; ++m) dma_round(u, m);
   };
-  const uint16_t* lane_off = lds + c * LD + 8 * g;
-  auto aread = [&](int u, int kt) {
-    const uint16_t* q = lane_off + (u % 3) * CH + 32 * kt;
+  // lane (row c, group g): k-step kt reads logical slot 4kt + g of row c in
+  // plane p of buffer u%3 = abase[kt] + (u%3)·2CH + p·PLB bytes
+  uint32_t abase[KT];
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+    abase[kt] = lds_addr(ring) + 2 * (c * KC + 8 * ((4 * kt + g) ^ (c & SWM)));
+  auto aread = [&](auto uc, auto ktc) {
+    constexpr int OFF = (decltype(uc)::value % 3) * 2 * CH;
+    constexpr int kt = decltype(ktc)::value;
     S8 r;
-    r.h = *reinterpret_cast<const u4*>(q);
-    r.m = *reinterpret_cast<const u4*>(q + PL);
-    r.l = *reinterpret_cast<const u4*>(q + 2 * PL);
+    r.h = ds_read16<OFF>(abase[kt]);
+    r.m = ds_read16<OFF + PLB>(abase[kt]);
+    if constexpr (OFF + 2 * PLB < 65536) r.l = ds_read16<OFF + 2 * PLB>(abase[kt]);
+    else r.l = ds_read16<OFF + PLB>(abase[kt] + PLB);
     return r;
   };
-#pragma unroll
-  for (int j = 0; j < 2 && j < U; ++j) {
-    gload(j);
-    lput(j);
-  }
-  __syncthreads();
+  auto lgkm_wait = [](S8& r) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.h), "+v"(r.m), "+v"(r.l));
+  };
+  // Retire sub-chunk u+1's DMA, which is older than every vm op issued in
+  // iteration u: [flush stores][pre loads][DMA(u+2)].  Those may stay in flight,
+  // so the wait leaves exactly their count outstanding (NST / NLD are the exact
+  // store / load instructions of flush / pre, or fewer: fewer only over-waits).
+  // Stores thereby get two iterations to be acknowledged instead of one.
+  auto vm_wait_barrier = [&](auto nc) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(nc)::value));
+    asm volatile("s_waitcnt lgkmcnt(0)");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  dma(0);
+  if (U > 1) dma(1);
+  vm_wait_barrier(std::integral_constant<int, (U > 1 ? NDMA : 0)>{});
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-  S8 a_cur = aread(0, 0);
+  S8 a_cur = aread(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  lgkm_wait(a_cur);
   f4 acc_prev = zero4, pv_prev = zero4, pv = zero4, hi = zero4, lo = zero4;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int J = u / NH, hh = u % NH;
-    if (hh == 0) {
-      if (J >= 2) flush(J - 2);
+  static_for<0, U>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    constexpr int J = u / NH, hh = u % NH;
+    if constexpr (hh == 0) {
+#ifndef NERFHIP_EXP_NOFLUSH
+      if constexpr (J >= 2) flush(J - 2);
+#endif
       hi = zero4;
       lo = zero4;
+      pv = pre(J);
     }
-    if (u + 2 < U) gload(u + 2);
-    if (hh == 0) pv = pre(J);
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
+    __builtin_amdgcn_sched_barrier(0);   // flush / pre before the DMA: vmcnt counts in order
+    const unsigned long long t_d0 = MEMTIME();
+    // (one DMA round per k-step instead measured slower: the issue stall
+    // moved into the k-steps and the end-of-sub-chunk wait grew)
+#ifndef NERFHIP_EXP_NOSTAGE
+    if constexpr (u + 2 < U) dma(u + 2);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t_d1 = MEMTIME();
+    static_for<0, KT>([&](auto ktc) {
+      constexpr int kt = decltype(ktc)::value;
       S8 a_nxt = a_cur;
-      if (kt + 1 < KT) a_nxt = aread(u, kt + 1);
-      else if (u + 1 < U) a_nxt = aread(u + 1, 0);
+      if constexpr (kt + 1 < KT) a_nxt = aread(uc, std::integral_constant<int, kt + 1>{});
       mfma16x3(a_cur, b[hh * KT + kt], hi, lo);
-      if (hh == 0 && J > 0) {
+      if constexpr (hh == 0 && J > 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int kq = 1 + q * QSTEP < KT ? 1 + q * QSTEP : KT - 1;
           if (kt == kq) elem(J - 1, q, acc_prev[q], pv_prev[q]);
         }
       }
+      if constexpr (kt + 1 < KT) lgkm_wait(a_nxt);
       __builtin_amdgcn_sched_barrier(0);
       a_cur = a_nxt;
-    }
-    if (hh == NH - 1) {
+    });
+    if constexpr (hh == NH - 1) {
       acc_prev = hi + lo;
       pv_prev = pv;
     }
-    if (u + 2 < U) lput(u + 2);
-    __syncthreads();
-  }
+    const unsigned long long t_w0 = MEMTIME();
+#ifndef NERFHIP_EXP_NOBARRIER
+    constexpr int n_out = (u + 2 < U ? NDMA : 0) + (hh == 0 ? NLD : 0) +
+                          (hh == 0 && J >= 2 ? NST : 0);
+    vm_wait_barrier(std::integral_constant<int, n_out>{});   // sub-chunk u+1 landed everywhere
+#endif
+#ifdef NERFHIP_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)");
+    const unsigned long long t_w1 = MEMTIME();
+    STAMP_ADD(8, t_d1 - t_d0);     // DMA issue
+    STAMP_ADD(9, t_w0 - t_d1);     // k-steps (MFMA + epilogue VALU + LDS reads)
+    STAMP_ADD(10, t_w1 - t_w0);    // vm wait + barrier (+ drain, diagnostic only)
+    STAMP_ADD(11, 1);              // sub-chunks
+#else
+    (void)t_d0; (void)t_d1; (void)t_w0;
+#endif
+    if constexpr (u + 1 < U) {           // its first fragment, only now readable
+      a_cur = aread(std::integral_constant<int, u + 1>{}, std::integral_constant<int, 0>{});
+      lgkm_wait(a_cur);
+    }
+  });
   if (JT >= 2) flush(JT - 2);
 #pragma unroll
   for (int q = 0; q < 4; ++q) elem(JT - 1, q, acc_prev[q], pv_prev[q]);
@@ -527,14 +627,16 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
 }
 
 // one GEMM phase in the kernel's precision (B: float[K/16][4] or S8[K/32])
-template <bool X3, int K, int JT, class B, class Pre, class Elem, class Flush>
-__device__ __forceinline__ void gemm_any(const void* src, float* lds, const B& b, int tid, int c,
-                                         int g, Pre&& pre, Elem&& elem, Flush&& flush) {
+template <bool X3, int K, int JT, int NTH, int NST, int NLD, class B, class Pre, class Elem,
+          class Flush>
+__device__ __forceinline__ void gemm_any(const void* src, float* lds, uint16_t* ring, const B& b,
+                                         int tid, int c, int g, Pre&& pre, Elem&& elem,
+                                         Flush&& flush) {
   if constexpr (X3)
-    gemm_phase_x3<K, JT>(static_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(lds), b,
-                         tid, c, g, pre, elem, flush);
+    gemm_phase_x3<K, JT, NTH, NST, NLD>(static_cast<const uint16_t*>(src), ring, b, tid, c, g, pre, elem,
+                         flush);
   else
-    gemm_phase<K, JT>(static_cast<const float*>(src), lds, b, tid, c, g, pre, elem, flush);
+    gemm_phase<K, JT, NTH>(static_cast<const float*>(src), lds, b, tid, c, g, pre, elem, flush);
 }
 
 template <bool C, class A, class B>
@@ -552,23 +654,31 @@ __device__ __forceinline__ void stage_vec(float* dst, const float* src, int n, i
 // W/NSPLIT features; all passes but the last park their fragments in a
 // per-wave LDS stash.  Live output registers drop from W/4 to W/(4·NSPLIT),
 // which is what lets W = 512 fit the 256 VALU-addressable VGPRs.
+// Rows per workgroup: 16 per wave.  (8 waves = 128 rows per workgroup at W = 256
+// halves the weight staging per row but measured no faster: 1.98 vs 2.03 ms
+// bf16x3, 2.88 vs 2.70 ms fp32 for the 160-fit medium group.)
 template <int W> struct RowsCfg {
   static constexpr int NSPLIT = W >= 512 ? 2 : 1;
   static constexpr int WAVES_PER_SIMD = W >= 512 ? 1 : 2;
+  static constexpr int NWAVES = 4;
+  static constexpr int THREADS = 64 * NWAVES, ROWS = 16 * NWAVES;
 };
 
-template <int W, int D, bool X3>
-__global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_rows(KArgs a) {
+template <int W, int D, bool X3, bool TRAIN>
+__global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIMD)
+    k_step_rows(KArgs a) {
+  constexpr int NWV = RowsCfg<W>::NWAVES, NTH = RowsCfg<W>::THREADS;
   constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
   constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
   constexpr int WBUF_F = phase_lds_floats<W>() > phase_lds_floats<D>()
                              ? phase_lds_floats<W>() : phase_lds_floats<D>();
-  constexpr int WBUF = X3 ? x3_lds_halfs<KMAX>() / 2 : WBUF_F;   // weight ring, in floats
+  constexpr int WBUF = X3 ? 0 : WBUF_F;   // fp32 weight ring, in floats (bf16x3: xring)
   constexpr int STASH = (NS - 1) * JP * 256;                // per wave
-  __shared__ __attribute__((aligned(16))) float lds[WBUF + 2 * KMAX + 4 * STASH];
+  __shared__ __attribute__((aligned(16))) float lds[WBUF + 2 * KMAX + NWV * STASH];
+  __shared__ __attribute__((aligned(16))) uint16_t xring[X3 ? x3_ring_halfs<KMAX>() : 8];
   float* bias = lds + WBUF;   // a phase's bias, or w0 ‖ b0 in the layer-0 backward
   int fit, tile;
-  if (!map_block(blockIdx.x, a.n_fits, a.n_pad / kRowsPerBlock, fit, tile)) return;
+  if (!map_block(blockIdx.x, a.n_fits, a.n_pad / RowsCfg<W>::ROWS, fit, tile)) return;
   STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -577,10 +687,10 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   const int L = a.fit_layers[fit];
   const float om = a.fit_omega[fit];
   const int n_pad = a.n_pad;
-  const int rblk = tile * 4 + wave;           // 16-row block
+  const int rblk = tile * NWV + wave;         // 16-row block
   const int r = rblk * 16 + c;                // this lane's row (B/D column)
   const bool valid = r < a.N;
-  const bool train = a.mode == 0;
+  constexpr bool train = TRAIN;   // a.mode == 0
 
   const float* P = a.params + fit * a.p_stride;
   const float* PT = a.params_t + fit * a.pt_stride;
@@ -613,12 +723,14 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   // Run a W-wide output layer as NS passes over src rows; out(Jg, q, acc, pv)
   // writes element q of feature tile Jg into ho[Jg % JP], flush(Jg) stores
   // the tile; afterwards hb ← output.
-  auto wide_layer = [&](const void* src, auto& bop, auto&& pre, auto&& out, auto&& flush) {
+  // nst / nld: the exact vm store / load counts of flush / pre (bf16x3 waits)
+  auto wide_layer = [&](auto nst, auto nld, const void* src, auto& bop, auto&& pre, auto&& out,
+                        auto&& flush) {
     constexpr int K = (sizeof(bop) / sizeof(bop[0])) * (X3 ? 32 : 16);
 #pragma unroll
     for (int p = 0; p < NS; ++p) {
-      gemm_any<X3, K, JP>(
-          static_cast<const char*>(src) + (int64_t)p * JP * K * (X3 ? 96 : 64), lds, bop, tid,
+      gemm_any<X3, K, JP, NTH, decltype(nst)::value, decltype(nld)::value>(
+          static_cast<const char*>(src) + (int64_t)p * JP * K * (X3 ? 96 : 64), lds, xring, bop, tid,
           c, g, [&](int J) { return pre(p * JP + J); },
           [&](int J, int q, float acc, float pv) { out(p * JP + J, q, acc, pv); },
           [&](int J) { flush(p * JP + J); });
@@ -693,7 +805,7 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
     f4 cs_pend;
     wide_layer(
-        wsrc(false, i), hb, no_pre,
+        ic<TRAIN ? 5 : 0>, ic<0>, wsrc(false, i), hb, no_pre,
         [&](int J, int q, float acc, float) {
           const float z = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
           float s, co;
@@ -720,8 +832,8 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
   S8 ys[JD / 2];
   float sq = 0.f;
   f4 y_pend;
-  gemm_any<X3, W, JD>(
-      wsrc(false, L + 1), lds, hb, tid, c, g,
+  gemm_any<X3, W, JD, NTH, TRAIN ? 4 : 0, TRAIN ? 1 : 0>(
+      wsrc(false, L + 1), lds, xring, hb, tid, c, g,
       [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
       [&](int J, int q, float acc, float t) {
         y_pend[q] = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
@@ -765,13 +877,14 @@ __global__ void __launch_bounds__(kThreads, RowsCfg<W>::WAVES_PER_SIMD) k_step_r
     for (int J2 = 0; J2 < JD / 2; ++J2) ys[J2] = split_pair(y[2 * J2], y[2 * J2 + 1]);
   }
   auto& yb = pick_ref<X3>(ys, y);
-  wide_layer(wsrc(true, L + 1), yb, cos_pre(L), dz_out, dz_store(L));   // W_fᵀ [W][D]
+  wide_layer(ic<4>, ic<1>, wsrc(true, L + 1), yb, cos_pre(L), dz_out,
+             dz_store(L));   // W_fᵀ [W][D]
   STAMP(4);
   for (int i = L; i >= 2; --i)
-    wide_layer(wsrc(true, i), hb, cos_pre(i - 1), dz_out, dz_store(i - 1));
+    wide_layer(ic<4>, ic<1>, wsrc(true, i), hb, cos_pre(i - 1), dz_out, dz_store(i - 1));
   // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op sequence
   stage_vec(bias, P, 2 * W, tid);   // visible after gemm_phase's prologue barrier
-  wide_layer(wsrc(true, 1), hb, no_pre,
+  wide_layer(ic<4>, ic<0>, wsrc(true, 1), hb, no_pre,
              [&](int K, int q, float acc, float) {
                const int f = 16 * K + 4 * g + q;
                const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
@@ -1361,7 +1474,7 @@ int validate(int W, int D, int N, int L_max, int epochs) {
 }
 
 void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
-  const int64_t n_pad = ((int64_t)N + kRowsPerBlock - 1) / kRowsPerBlock * kRowsPerBlock;
+  const int64_t n_pad = ((int64_t)N + kRowPad - 1) / kRowPad * kRowPad;
   s->n_pad = n_pad;
   s->params = n_params(W, D, L_max);
   s->params_t = (int64_t)L_max * W * W + (int64_t)W * D;
@@ -1405,8 +1518,13 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
 
 template <int W, int D, bool X3>
 int launch_rows(const KArgs& a, hipStream_t st) {
-  const int grid = grid_for(a.n_fits, a.n_pad / kRowsPerBlock);
-  hipLaunchKernelGGL((k_step_rows<W, D, X3>), dim3(grid), dim3(kThreads), 0, st, a);
+  const int grid = grid_for(a.n_fits, a.n_pad / RowsCfg<W>::ROWS);
+  if (a.mode == 0)
+    hipLaunchKernelGGL((k_step_rows<W, D, X3, true>), dim3(grid), dim3(RowsCfg<W>::THREADS), 0,
+                       st, a);
+  else
+    hipLaunchKernelGGL((k_step_rows<W, D, X3, false>), dim3(grid), dim3(RowsCfg<W>::THREADS), 0,
+                       st, a);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 

@@ -36,9 +36,13 @@ def test_header_symbols_exported(lib):
         assert getattr(lib, n)
 
 
-def test_code_object_is_gfx950(lib):
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading",
-                          str(_build.LIB)], capture_output=True, text=True, cwd="/tmp")
+def test_code_object_is_gfx950(lib, tmp_path):
+    # --offloading extracts the bundles next to its input: work on a copy
+    import shutil
+    so = tmp_path / "lib.so"
+    shutil.copy(_build.LIB, so)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(so)],
+                         capture_output=True, text=True, cwd=tmp_path)
     assert "gfx950" in (out.stdout + out.stderr)
 
 
@@ -51,7 +55,7 @@ def test_abi_and_status(lib):
 @pytest.mark.parametrize("W,D,N,L,E", [(256, 128, 2048, 3, 2000), (64, 64, 130, 1, 5)])
 def test_group_sizes(lib, W, D, N, L, E):
     s = _native.group_sizes(W, D, N, L, E)
-    n_pad = (N + 63) // 64 * 64
+    n_pad = (N + 63) // 64 * 64       # whole 64-row workgroups
     assert s.n_pad == n_pad
     assert s.params == 2 * W + L * (W * W + W) + W * D + D
     assert s.params_t == L * W * W + W * D

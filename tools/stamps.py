@@ -33,16 +33,15 @@ torch.manual_seed(0)
 specs = [engine.FitSpec(keys, cfg, SIREN(cfg, 128).flat_parameters()) for _ in range(args.fits)]
 job = engine.FitJob(specs, args.epochs, devices=[0], precision=args.precision)
 g = job.groups[0]
-n_tiles = g.n_pad // 64
-blocks = 8 * n_tiles * ((g.n + 7) // 8)
-buf = torch.zeros(blocks * 4 * 8, dtype=torch.int64, device="cuda")
+n_waves = 8 * ((g.n + 7) // 8) * (g.n_pad // 16)    # every wave of the grid, any rows/WG
+buf = torch.zeros(n_waves * 16, dtype=torch.int64, device="cuda")
 lib = _native.load()
 lib.nerfhip_debug_set_stamps.argtypes = [ctypes.c_void_p]
 assert lib.nerfhip_debug_set_stamps(buf.data_ptr()) == 0
 job.launch()
 job.wait()
-st = buf.view(blocks, 4, 8).cpu().numpy().astype(np.float64)
-st = st[st[:, :, 0] > 0]                      # waves that ran (mapped blocks)
+st = buf.view(n_waves, 16).cpu().numpy().astype(np.float64)
+st = st[st[:, 0] > 0]                         # waves that ran (mapped blocks)
 d = np.diff(st[:, :6], axis=1)
 W, L, D = cfg.hidden_features, cfg.hidden_layers, 128
 mf = {"layer0": 0, "hidden_fwd": L * (W // 16) * (W // 16) * 4, "final_fwd": (D // 16) * (W // 16) * 4,
@@ -56,5 +55,10 @@ for i, name in enumerate(mf):
                  "mfma_pipe_cycles": mf[name] * cyc,
                  "ratio": round(float(d[:, i].mean()) / max(1, mf[name] * cyc), 3)}
 out["total_cycles"] = round(float((st[:, 5] - st[:, 0]).mean()))
+if st[:, 11].sum() > 0:   # bf16x3 phase counters (per wave, summed over sub-chunks)
+    out["x3_phase"] = {"subchunks": round(float(st[:, 11].mean()), 1),
+                       "dma_issue": round(float(st[:, 8].mean())),
+                       "ksteps": round(float(st[:, 9].mean())),
+                       "wait_barrier": round(float(st[:, 10].mean()))}
 out["waves"] = int(st.shape[0])
 print(json.dumps(out, indent=1))
