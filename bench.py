@@ -8,9 +8,20 @@ fits are split over the ranks by longest-processing-time on their FLOP cost —
 no collective touches the data path; a barrier and a max-over-ranks of the
 elapsed time bracket the timed steps.  value = 280·steps / max time.
 
+Precision (--precision, default bf16x3): the GEMMs run either on the exact
+f32 MFMA ("fp32") or as exact 3-way bf16 splits with six bf16 MFMA products
+per fp32 product and fp32 accumulation ("bf16x3": fp32-class accuracy,
+nerfhip.h nerfhip_precision); everything else is fp32 in both.  Both are held
+to the same per-fit parity bar (cos_delta_vs_ref).  With --also-fp32 (default
+on at N=1) the line also carries one timed fp32 sweep.
+
 Also reported (rank 0):
   roofline      the dominant kernel's algorithmic TFLOP/s (hipEvent-timed over
-                the timed steps) against the gfx950 FP32 MFMA peak;
+                the timed steps, while the width groups run concurrently)
+                against the matrix-core peak of its arithmetic: 157.3 TFLOP/s
+                f32 MFMA, or 2.5 PFLOP/s bf16 dense / 6 products = 416.7
+                TFLOP/s fp32-equivalent for bf16x3; plus the same kernel timed
+                alone for 20 epochs after the timed region ("isolated");
   cpu_baseline  the oracle (CPU restatement of the reference loop) timed on a
                 bounded sample of the same workload on this host (N=1 only);
   cos_delta_vs_ref  per-fit |Δ final_cosine_mean| against the reference's own
@@ -35,6 +46,8 @@ import torch
 import torch.distributed as dist
 
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4
+BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 (no sparsity)
+PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 6}
 RTX4060_FITS_PER_S = 0.232         # BASELINE.md §1 (280 fits / Σ train_time_seconds)
 GOLDEN_SWEEP = ROOT / "tests" / "golden" / "sweep_ref_seed0_e2000.json"
 PMC_TRAFFIC = ROOT / "profiles" / "pmc_traffic.json"
@@ -83,6 +96,41 @@ def cpu_baseline(seq_len: int, sample_epochs: int) -> dict:
             "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()}}
 
 
+def isolated_kernel(gspecs, kname, flops, precision, peak, device, epochs=20) -> dict:
+    """The dominant kernel's group trained alone (no concurrent groups) for a
+    few epochs, after the timed region: its undisturbed launch time."""
+    from nerf_attention import engine
+    job = engine.FitJob(gspecs, epochs, devices=[device], precision=precision)
+    job.launch(timed=True)
+    job.wait()
+    t = job.timing[0]
+    ms = (t.rows_ms if "rows" in kname else t.params_ms) / t.launches
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"avg_launch_ms": round(ms, 4), "achieved": round(tf, 2), "frac": round(tf / peak, 4),
+            "frac_of_f32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "epochs": epochs}
+
+
+def fp32_sweep(specs, epochs, device, plan, ref_cos, n_total) -> dict:
+    """One timed sweep on the exact f32 MFMA path (same fits, same parity bar)."""
+    from nerf_attention import engine
+    job = engine.FitJob(specs, epochs, devices=[device], precision="fp32")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    job.launch()
+    job.wait()
+    dt = time.perf_counter() - t0
+    out = {"value": round(len(specs) / dt, 4), "unit": "fits/s", "ms_per_step": round(dt * 1e3, 2),
+           "note": "one sweep, first launch of this job (no warm-up)"}
+    if ref_cos is not None and GOLDEN_SWEEP.exists():
+        ref = {r["name"]: r["final_cosine_mean"]
+               for r in json.loads(GOLDEN_SWEEP.read_text())["records"]}
+        d = np.array([abs(float(torch.from_numpy(o.row_cos).mean()) - ref[plan[i][0]])
+                      for i, o in enumerate(job.outputs())])
+        out["cos_delta_vs_ref"] = {"max": float(d.max()), "mean": float(d.mean()),
+                                   "within_1e-3": int((d <= 1e-3).sum()), "n": int(d.size)}
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,7 +141,10 @@ def main() -> None:
     ap.add_argument("--cpu-sample-epochs", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"])
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"])
+    ap.add_argument("--also-fp32", dest="also_fp32", action="store_true", default=None,
+                    help="also time one fp32 sweep (default: on at N=1 with bf16x3)")
+    ap.add_argument("--no-also-fp32", dest="also_fp32", action="store_false")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,17 +204,29 @@ def main() -> None:
             achieved = flops / (avg_ms * 1e-3) / 1e12
             traffic = None
             if PMC_TRAFFIC.exists():
-                traffic = json.loads(PMC_TRAFFIC.read_text()).get(kname)
+                traffic = json.loads(PMC_TRAFFIC.read_text()).get(f"{kname}[{args.precision}]")
             step_flops = sum(engine.fit_flops(N, 128, specs[i].config, args.epochs)
                              for i in mine)
+            peak = PEAK[args.precision]
+            job_tf = step_flops / (t_max / args.steps) / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 3),
-                    "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "kernel": kname, "fits_per_launch": g.n, "avg_launch_ms": round(avg_ms, 4),
-                    "flops_per_launch": flops,
+                    "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "kernel": f"{kname} [{args.precision}]", "fits_per_launch": g.n,
+                    "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": flops,
+                    "flops_unit": "algorithmic fp32 GEMM FLOPs (2 per multiply-add), "
+                                  "SURVEY.md §8d",
+                    "peak_basis": ("f32 MFMA" if args.precision == "fp32" else
+                                   "bf16 MFMA 2.5 PF dense / 6 bf16 products per fp32 product"),
                     "note": "launch durations measured while the width groups run concurrently",
                     "kernels_avg_ms": {c[1]: round(c[2], 4) for c in cands},
-                    "job_achieved_tflops": round(step_flops / (t_max / args.steps) / 1e12, 2)}
+                    "job_achieved_tflops": round(job_tf, 2),
+                    "job_frac": round(job_tf / peak, 4),
+                    "job_frac_of_f32_mfma_peak": round(job_tf / FP32_MFMA_PEAK_TFLOPS, 4)}
+            if world == 1:
+                roof["isolated"] = isolated_kernel(
+                    [specs[mine[i]] for i in g.members], kname, flops, args.precision, peak,
+                    local)
         parity = None
         if GOLDEN_SWEEP.exists() and args.epochs == 2000 and args.seq_len == 2048:
             ref = json.loads(GOLDEN_SWEEP.read_text())["records"]
@@ -178,7 +241,8 @@ def main() -> None:
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(value / RTX4060_FITS_PER_S, 2),
-            "dtype": "f32", "data": "synthetic",
+            "dtype": "f32" if args.precision == "fp32" else "f32 (bf16x3 split MFMA)",
+            "precision": args.precision, "data": "synthetic",
             "config": {"workload": "280-fit sweep: 7 archs x layers{0,8,16,24,31} x heads0-3 x "
                                    "K/V on the reference's synthetic KV (32x8xNx128), "
                                    "seed-0 inits in reference order",
@@ -187,6 +251,10 @@ def main() -> None:
             "roofline": roof,
             "cos_delta_vs_ref": parity,
         }
+        also = args.also_fp32 if args.also_fp32 is not None else args.precision != "fp32"
+        if world == 1 and also:
+            line["fp32_mfma"] = fp32_sweep([specs[i] for i in mine], args.epochs, local, plan,
+                                           all_cos if parity else None, n_total)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.seq_len, args.cpu_sample_epochs)
         print(json.dumps(line), flush=True)

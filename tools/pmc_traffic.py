@@ -20,8 +20,12 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    m = re.search(r"(k_\w+)<(\d+), (\d+)>", name)
-    return f"{m.group(1)}<{m.group(2)},{m.group(3)}>" if m else name.split("(")[0][-40:]
+    """k_step_rows<512, 128, true, true> -> k_step_rows<512,128>[bf16x3]"""
+    m = re.search(r"(k_\w+)<(\d+), (\d+)(?:, (true|false))?", name)
+    if not m:
+        return name.split("(")[0][-40:]
+    prec = "[bf16x3]" if m.group(4) == "true" else "[fp32]"
+    return f"{m.group(1)}<{m.group(2)},{m.group(3)}>{prec}"
 
 
 def per_launch(path: str, counter: str) -> dict:
