@@ -49,10 +49,16 @@ typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-namespace {
+// Build split: the library is compiled as NERFHIP_PART = 0 (host ABI + small
+// kernels) and one part per (hidden width, precision) (1..8 = W 64, 128, 256,
+// 512 × fp32, bf16x3: those step kernels, both head dims), in parallel, and
+// linked; without NERFHIP_PART the file is one translation unit.  Only KArgs
+// and the launch templates have external linkage (nerfhip_detail).
+#ifndef NERFHIP_PART
+#define NERFHIP_PART (-1)
+#endif
 
-constexpr int kRowPad = 64;    // n_pad granule: a whole number of row workgroups
-
+namespace nerfhip_detail {
 struct KArgs {
   int32_t W, D, N, n_pad, n_fits, L_max, epochs, epoch, mode;
   int64_t p_stride, pt_stride, s_stride, t_stride, lp_stride, y_stride;
@@ -83,6 +89,16 @@ struct KArgs {
   int64_t ws_stride;
   uint16_t* wsplit;
 };
+template <int W, int D, bool X3> int launch_rows(const KArgs& a, hipStream_t st);
+template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t st);
+}  // namespace nerfhip_detail
+
+namespace {
+using nerfhip_detail::KArgs;
+
+constexpr int kRowPad = 64;    // n_pad granule: a whole number of row workgroups
+
+
 
 #ifdef NERFHIP_STAMPS
 // Diagnostic build only (tools/stamps.py): per-wave s_memtime stamps at the
@@ -1516,6 +1532,9 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
 }
 
 
+}  // namespace
+
+namespace nerfhip_detail {
 template <int W, int D, bool X3>
 int launch_rows(const KArgs& a, hipStream_t st) {
   const int grid = grid_for(a.n_fits, a.n_pad / RowsCfg<W>::ROWS);
@@ -1539,6 +1558,45 @@ int launch_params(const KArgs& a, hipStream_t st) {
   }
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
+
+#define NERFHIP_INST_ONE(W, D, X) \
+  template int launch_rows<W, D, X>(const KArgs&, hipStream_t); \
+  template int launch_params<W, D, X>(const KArgs&, hipStream_t);
+#define NERFHIP_INST(W, X) NERFHIP_INST_ONE(W, 64, X) NERFHIP_INST_ONE(W, 128, X)
+#if NERFHIP_PART == 1
+NERFHIP_INST(64, false)
+#elif NERFHIP_PART == 2
+NERFHIP_INST(64, true)
+#elif NERFHIP_PART == 3
+NERFHIP_INST(128, false)
+#elif NERFHIP_PART == 4
+NERFHIP_INST(128, true)
+#elif NERFHIP_PART == 5
+NERFHIP_INST(256, false)
+#elif NERFHIP_PART == 6
+NERFHIP_INST(256, true)
+#elif NERFHIP_PART == 7
+NERFHIP_INST(512, false)
+#elif NERFHIP_PART == 8
+NERFHIP_INST(512, true)
+#elif NERFHIP_PART == 0
+#define NERFHIP_EXTERN_ONE(W, D, X) \
+  extern template int launch_rows<W, D, X>(const KArgs&, hipStream_t); \
+  extern template int launch_params<W, D, X>(const KArgs&, hipStream_t);
+#define NERFHIP_EXTERN(W) \
+  NERFHIP_EXTERN_ONE(W, 64, false) NERFHIP_EXTERN_ONE(W, 64, true) \
+  NERFHIP_EXTERN_ONE(W, 128, false) NERFHIP_EXTERN_ONE(W, 128, true)
+NERFHIP_EXTERN(64)
+NERFHIP_EXTERN(128)
+NERFHIP_EXTERN(256)
+NERFHIP_EXTERN(512)
+#endif
+}  // namespace nerfhip_detail
+
+#if NERFHIP_PART <= 0
+namespace {
+using nerfhip_detail::launch_params;
+using nerfhip_detail::launch_rows;
 
 typedef int (*launch_fn)(const KArgs&, hipStream_t);
 
@@ -1801,3 +1859,4 @@ int nerfhip_siren_forward(const nerfhip_group* g, void* stream) {
 }
 
 }  // extern "C"
+#endif  // NERFHIP_PART <= 0

@@ -32,13 +32,33 @@ def _stale() -> bool:
     return any(p.stat().st_mtime > t for p in SOURCES + HEADERS)
 
 
+N_PARTS = 9   # NERFHIP_PART 0 = host ABI + small kernels, 1..8 = (W, precision) kernels
+
+
 def build(force: bool = False, verbose: bool = True) -> Path:
+    """Compile the nine NERFHIP_PART translation units in parallel (one per
+    hidden width × precision + the host part), then link them into
+    libnerfhip.so."""
     if not force and not _stale():
         return LIB
     LIB_DIR.mkdir(parents=True, exist_ok=True)
+    obj_dir = LIB_DIR / "obj"
+    obj_dir.mkdir(exist_ok=True)
+    base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            "-Wno-unused-function", "-I", str(INCLUDE)]
+    objs, procs = [], []
+    for part in range(N_PARTS):
+        obj = obj_dir / f"nerfhip_p{part}.o"
+        cmd = base + [f"-DNERFHIP_PART={part}", "-c", str(SOURCES[0]), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr, flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    failed = [p.args for p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
     tmp = LIB.with_suffix(".so.tmp")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", "-I", str(INCLUDE), "-o", str(tmp), *map(str, SOURCES)]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr, flush=True)
     subprocess.run(cmd, check=True)
