@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -105,7 +106,7 @@ SPLIT_MAX_FITS = 8   # libnerfhip splits the gradient reduction of groups below 
 #            products per pair, fp32 accumulation: fp32-class accuracy at 2.7x
 #            the matrix-core rate.
 PRECISIONS = tuple(_native.PRECISIONS)
-DEFAULT_PRECISION = "fp32"
+DEFAULT_PRECISION = os.environ.get("NERFHIP_PRECISION", "bf16x3")
 
 
 def check_precision(precision):

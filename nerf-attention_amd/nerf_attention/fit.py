@@ -75,7 +75,7 @@ def sweep_plan(layers, heads, configs, load_layer):
     return plan, skipped
 
 
-def train_plan(plan, epochs: int, devices, log_every: int):
+def train_plan(plan, epochs: int, devices, log_every: int, precision=None):
     """Initialise every model in plan order (the reference's RNG order), then
     train them all on the engine.  Returns [(FitResult, probes)]."""
     models, specs = [], []
@@ -83,7 +83,8 @@ def train_plan(plan, epochs: int, devices, log_every: int):
         m = SIREN(cfg, out_features=int(tensor.shape[1]))
         models.append(m)
         specs.append(engine.FitSpec(target=tensor, config=cfg, init=m.flat_parameters()))
-    outs = engine.run_fits(specs, epochs, log_every=log_every, devices=devices)
+    outs = engine.run_fits(specs, epochs, log_every=log_every, devices=devices,
+                           precision=precision)
     results = []
     for (name, _l, _h, _kv, cfg, tensor), m, o in zip(plan, models, outs):
         m = m.to(torch.device('cuda', o.device))
@@ -104,10 +105,12 @@ def fit_kv_cache(
     gpus: int | None = None,
     select: str = 'sweep',
     configs=None,
+    precision: str | None = None,
 ) -> list[dict]:
     """Fit SIRENs to an extracted KV cache and record metrics (fit.py:20-92).
     Extensions: `gpus` farms the fits over this many local GPUs; `select` and
-    `configs` widen / narrow the selection (see select_fits)."""
+    `configs` widen / narrow the selection (see select_fits); `precision` picks
+    the GEMM arithmetic (engine.PRECISIONS)."""
     kv_dir, output_dir = Path(kv_dir), Path(output_dir)
     output_dir.mkdir(parents=True, exist_ok=True)
     with open(kv_dir / 'metadata.json') as f:
@@ -130,7 +133,8 @@ def fit_kv_cache(
         return torch.load(p, map_location='cpu', weights_only=True)
 
     plan, skipped = sweep_plan(layers, heads, configs, load_layer)
-    results = train_plan(plan, epochs, devices, log_every=max(epochs // 5, 100))
+    results = train_plan(plan, epochs, devices, log_every=max(epochs // 5, 100),
+                         precision=precision)
 
     all_results: list[dict] = []
     count = 0
@@ -242,6 +246,9 @@ def main() -> None:
                         help="'all' = every layer x every KV head (extension)")
     parser.add_argument('--configs', type=str, default=None,
                         help='comma-separated architecture names, e.g. medium or wide (extension)')
+    parser.add_argument('--precision', choices=['bf16x3', 'fp32'], default=None,
+                        help='GEMM arithmetic (extension; default bf16x3 = exact 3-way bf16 '
+                             'split, fp32-class; fp32 = f32 MFMA)')
     args = parser.parse_args()
     if args.seed is not None:
         torch.manual_seed(args.seed)
@@ -250,7 +257,8 @@ def main() -> None:
     t0 = time.time()
     fit_kv_cache(Path(args.kv_dir), Path(args.output_dir), args.epochs, args.device,
                  args.quick, gpus=args.gpus, select=args.select,
-                 configs=args.configs.split(',') if args.configs else None)
+                 configs=args.configs.split(',') if args.configs else None,
+                 precision=args.precision)
     print(f"\n[nerf-attention-amd] sweep wall clock {time.time() - t0:.2f}s")
 
 

@@ -162,19 +162,23 @@ def fit_siren(
     device: str = 'cuda',
     log_every: int = 500,
     verbose: bool = True,
+    *,
+    precision: str | None = None,
 ) -> FitResult:
     """Fit a SIREN to one (seq_len, d_head) KV tensor on the MI355X engine.
 
     Same contract as the reference (siren.py:70-149): the input is not
     mutated, the torch CPU RNG is consumed exactly once (model init), the
     result owns its model (on `device`) and CPU copies of mean/std/metrics.
+    Extension: `precision` ("bf16x3" default, or "fp32"; engine.PRECISIONS)
+    picks the GEMM arithmetic — both meet the same per-fit parity bar.
     """
     seq_len, d_head = kv_tensor.shape
     dev = engine.resolve_device(device)
     model = SIREN(config, out_features=d_head)
     spec = engine.FitSpec(target=kv_tensor, config=config, init=model.flat_parameters())
     out = engine.run_fits([spec], epochs, lr=lr, log_every=log_every if verbose else 0,
-                          devices=[dev.index])[0]
+                          devices=[dev.index], precision=precision)[0]
     model = model.to(dev)
     model.load_flat_parameters(out.params)
     model.eval()  # siren.py:119
