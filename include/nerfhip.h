@@ -157,6 +157,38 @@ int nerfhip_siren_fit_timed(const nerfhip_group* groups, int32_t n_groups,
  * target/mean/std/row_cos/row_sq are set).  SIREN.forward, siren.py:60-61. */
 int nerfhip_siren_forward(const nerfhip_group* g, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Truncated-SVD baseline (BASELINE config 5).
+ * Replaces the per-slice CPU loop of the reference's SVD experiment
+ * (nerf_attention/experiments/svd.py:43-75: torch.linalg.svd, rank-r
+ * reconstruction U_r diag(S_r) V_rᵀ, F.cosine_similarity per row, mean / min /
+ * std) for a batch of KV slices in one call: fp64 Gram, Jacobi
+ * eigen-solver, and the per-row cosine of every requested rank as
+ * ‖projection onto the top-r right singular vectors‖ / ‖row‖.
+ * ------------------------------------------------------------------------ */
+#define NERFHIP_SVD_MAX_RANKS 8
+
+typedef struct nerfhip_svd_batch {
+  int32_t n_tensors;       /* slices in the batch                              */
+  int32_t N;               /* rows per slice (seq_len), >= 2                    */
+  int32_t D;               /* columns (head_dim): 64 or 128                     */
+  int32_t n_ranks;         /* 1..NERFHIP_SVD_MAX_RANKS                          */
+  int32_t ranks[NERFHIP_SVD_MAX_RANKS];   /* (host) each in [1, min(N, D)]      */
+  int32_t max_sweeps;      /* Jacobi sweep cap (<= 0: 30)                       */
+  int32_t reserved;
+  const float* x;          /* [n_tensors][N][D] slices, row-major               */
+  double* gram;            /* [n_tensors][D][D] workspace                       */
+  double* evec;            /* [n_tensors][D][D] out: row k = k-th right singular
+                              vector (eigenvalues descending)                    */
+  double* eval;            /* [n_tensors][D] out: σ² descending                  */
+  int32_t* order;          /* [n_tensors][D] out: solver index of each σ²        */
+  float* row_cos;          /* [n_tensors][n_ranks][N] out: per-row cosine        */
+  double* stats;           /* [n_tensors][n_ranks][3] out: mean, min, std (N−1)  */
+} nerfhip_svd_batch;
+
+/* Enqueue the whole batch on `stream`; asynchronous like the fit entry points. */
+int nerfhip_svd_rank_metrics(const nerfhip_svd_batch* b, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,7 +18,7 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 LIB_DIR = PKG / "_lib"
 LIB = LIB_DIR / "libnerfhip.so"
-SOURCES = [CSRC / "nerfhip.hip"]
+SOURCES = [CSRC / "nerfhip.hip", CSRC / "nerfhip_svd.hip"]
 HEADERS = [INCLUDE / "nerfhip.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -50,6 +50,13 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     for part in range(N_PARTS):
         obj = obj_dir / f"nerfhip_p{part}.o"
         cmd = base + [f"-DNERFHIP_PART={part}", "-c", str(SOURCES[0]), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr, flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    for extra in SOURCES[1:]:                       # further translation units
+        obj = obj_dir / f"{extra.stem}.o"
+        cmd = base + ["-c", str(extra), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr, flush=True)
         procs.append(subprocess.Popen(cmd))

@@ -50,6 +50,17 @@ class NerfhipGroup(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in _GROUP_INTS] + [(n, c_void_p) for n in _GROUP_PTRS]
 
 
+SVD_MAX_RANKS = 8
+
+
+class NerfhipSvdBatch(ctypes.Structure):
+    _fields_ = ([(n, c_int32) for n in ("n_tensors", "N", "D", "n_ranks")]
+                + [("ranks", c_int32 * SVD_MAX_RANKS), ("max_sweeps", c_int32),
+                   ("reserved", c_int32)]
+                + [(n, c_void_p) for n in ("x", "gram", "evec", "eval", "order", "row_cos",
+                                          "stats")])
+
+
 class NerfhipTiming(ctypes.Structure):
     _fields_ = [("launches", c_int32), ("reserved", c_int32), ("rows_ms", ctypes.c_double),
                 ("params_ms", ctypes.c_double)]
@@ -65,6 +76,7 @@ SIGNATURES = {
     "nerfhip_siren_fit_timed": (c_int32, [POINTER(NerfhipGroup), c_int32, POINTER(c_void_p),
                                           POINTER(NerfhipTiming)]),
     "nerfhip_siren_forward": (c_int32, [POINTER(NerfhipGroup), c_void_p]),
+    "nerfhip_svd_rank_metrics": (c_int32, [POINTER(NerfhipSvdBatch), c_void_p]),
 }
 
 _lib = None

@@ -46,6 +46,40 @@ def single(cfg, seq_len, epochs, label):
                       "final_cosine_mean": r.final_cosine_mean}), flush=True)
 
 
+def svd_baseline(seq_len):
+    """Config 5's SVD rank-k baseline: the svd.py selection (layers 0/16/31 x
+    4 heads x K/V = 24 slices) at seq_len, all four target ratios, on the
+    engine; next to the reference's CPU op sequence (oracle) on one slice."""
+    import sys
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import svd_oracle
+    from nerf_attention.svd import rank_metrics, svd_rank
+    from nerf_attention.synthetic import kv_layer
+    sl = []
+    for layer in (0, 16, 31):
+        t = kv_layer(layer, seq_len, 32, 8, 128, heads=range(4))
+        for h in range(4):
+            sl += [t["keys"][h], t["values"][h]]
+    x = torch.stack(sl).cuda()
+    ranks = sorted({svd_rank(seq_len, 128, tc) for tc in (2.0, 4.0, 8.0, 16.0)})
+    rank_metrics(x[:2], ranks)                                   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = rank_metrics(x, ranks)
+    torch.cuda.synchronize()
+    gpu_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for r in ranks:
+        svd_oracle.slice_metrics(sl[0], r)
+    cpu_s = (time.perf_counter() - t0) * len(sl)
+    print(json.dumps({"config": "5 svd baseline", "seq_len": seq_len, "slices": len(sl),
+                      "ranks": ranks, "gpu_s": round(gpu_s, 4),
+                      "cpu_oracle_s_extrapolated": round(cpu_s, 2),
+                      "cpu_threads": torch.get_num_threads(),
+                      "mean_cos_per_rank": [round(float(v), 4)
+                                            for v in out["stats"][:, :, 0].mean(0)]}), flush=True)
+
+
 def scan(lens, epochs):
     for n in lens:
         t0 = time.perf_counter()
@@ -72,7 +106,7 @@ def scan(lens, epochs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="+", choices=["single", "wide", "scan"])
+    ap.add_argument("which", nargs="+", choices=["single", "wide", "scan", "svd"])
     ap.add_argument("--epochs", type=int, default=2000)
     ap.add_argument("--scan-lens", default="512,1024,2048,4096")
     args = ap.parse_args()
@@ -81,6 +115,8 @@ def main():
         single(medium, 2048, args.epochs, "2 single fit")
     if "wide" in args.which:
         single(CONFIG_WIDE, 8192, args.epochs, "5 wide SIREN")
+    if "svd" in args.which:
+        svd_baseline(8192)
     if "scan" in args.which:
         scan([int(x) for x in args.scan_lens.split(",")], args.epochs)
 
