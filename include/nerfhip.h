@@ -189,6 +189,31 @@ typedef struct nerfhip_svd_batch {
 /* Enqueue the whole batch on `stream`; asynchronous like the fit entry points. */
 int nerfhip_svd_rank_metrics(const nerfhip_svd_batch* b, void* stream);
 
+/* ------------------------------------------------------------------------
+ * KV structure analysis.  Replaces the per-dimension numpy
+ * loops of the reference's pre-fit analysis (nerf_attention/analyze.py:20-44,
+ * _analyze_tensor :61-71): for every sampled head dimension of every slice,
+ * the lag-0..max_lag autocorrelation of the centred column and the fraction
+ * of Hann-windowed rfft energy in the lowest 5/10/25/50 % of bins.  fp64.
+ * (The effective rank, analyze.py:47-58, uses nerfhip_svd_rank_metrics.)
+ * ------------------------------------------------------------------------ */
+#define NERFHIP_ANALYSIS_MAX_DIMS 64
+
+typedef struct nerfhip_kv_analysis_batch {
+  int32_t n_tensors;       /* slices                                            */
+  int32_t N;               /* rows per slice (seq_len), 2..8192                 */
+  int32_t D;               /* columns (head_dim)                                */
+  int32_t n_dims;          /* sampled dimensions, 1..NERFHIP_ANALYSIS_MAX_DIMS   */
+  int32_t max_lag;         /* 0..1023 (reference: 50)                           */
+  int32_t reserved;
+  int32_t dims[NERFHIP_ANALYSIS_MAX_DIMS];   /* (host) column indices          */
+  const float* x;          /* [n_tensors][N][D]                                  */
+  double* autocorr;        /* [n_tensors][n_dims][max_lag + 1] out               */
+  double* energy;          /* [n_tensors][n_dims][4] out: top 5/10/25/50 %       */
+} nerfhip_kv_analysis_batch;
+
+int nerfhip_kv_analysis(const nerfhip_kv_analysis_batch* a, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,7 +18,7 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 LIB_DIR = PKG / "_lib"
 LIB = LIB_DIR / "libnerfhip.so"
-SOURCES = [CSRC / "nerfhip.hip", CSRC / "nerfhip_svd.hip"]
+SOURCES = [CSRC / "nerfhip.hip", CSRC / "nerfhip_svd.hip", CSRC / "nerfhip_analysis.hip"]
 HEADERS = [INCLUDE / "nerfhip.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

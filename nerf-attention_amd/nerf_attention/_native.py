@@ -61,6 +61,15 @@ class NerfhipSvdBatch(ctypes.Structure):
                                           "stats")])
 
 
+ANALYSIS_MAX_DIMS = 64
+
+
+class NerfhipKvAnalysisBatch(ctypes.Structure):
+    _fields_ = ([(n, c_int32) for n in ("n_tensors", "N", "D", "n_dims", "max_lag", "reserved")]
+                + [("dims", c_int32 * ANALYSIS_MAX_DIMS)]
+                + [(n, c_void_p) for n in ("x", "autocorr", "energy")])
+
+
 class NerfhipTiming(ctypes.Structure):
     _fields_ = [("launches", c_int32), ("reserved", c_int32), ("rows_ms", ctypes.c_double),
                 ("params_ms", ctypes.c_double)]
@@ -77,6 +86,7 @@ SIGNATURES = {
                                           POINTER(NerfhipTiming)]),
     "nerfhip_siren_forward": (c_int32, [POINTER(NerfhipGroup), c_void_p]),
     "nerfhip_svd_rank_metrics": (c_int32, [POINTER(NerfhipSvdBatch), c_void_p]),
+    "nerfhip_kv_analysis": (c_int32, [POINTER(NerfhipKvAnalysisBatch), c_void_p]),
 }
 
 _lib = None

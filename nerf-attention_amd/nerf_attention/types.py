@@ -73,6 +73,29 @@ class KVMetadata:
         return cls(**{k: v for k, v in d.items() if k in known})
 
 
+@dataclass
+class LayerSummary:
+    """Per-layer averages of the KV structure analysis (reference types.py:66-74)."""
+    layer: int
+    avg_autocorr_k: float
+    avg_autocorr_v: float
+    avg_energy_10pct_k: float
+    avg_energy_10pct_v: float
+    avg_rank_ratio_k: float
+    avg_rank_ratio_v: float
+
+
+@dataclass
+class AnalysisResult:
+    """Result of `analyze_kv_cache` (reference types.py:77-84)."""
+    metadata: KVMetadata
+    layer_summaries: list
+    avg_autocorr_keys: float
+    avg_autocorr_values: float
+    avg_spectral_keys: float
+    avg_spectral_values: float
+
+
 CONFIGS_QUICK: list[SIRENConfig] = [
     SIRENConfig(128, 1, 30.0, 'small'),
     SIRENConfig(256, 2, 30.0, 'medium'),

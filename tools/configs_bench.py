@@ -80,6 +80,38 @@ def svd_baseline(seq_len):
                                             for v in out["stats"][:, :, 0].mean(0)]}), flush=True)
 
 
+def analysis(seq_len):
+    """Pre-fit KV structure analysis (analyze.py selection: layers 0/8/16/24/31
+    x 4 heads x K/V = 40 slices) at seq_len on the engine, next to the
+    reference's CPU op sequence (oracle) on two slices, extrapolated."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import analysis_oracle
+    from nerf_attention.analyze import analyze_slices, select_layers
+    from nerf_attention.synthetic import kv_layer
+    sl, names = [], []
+    for layer in select_layers(32):
+        t = kv_layer(layer, seq_len, 32, 8, 128, heads=range(4))
+        for h in range(4):
+            sl += [t["keys"][h], t["values"][h]]
+            names += [f"L{layer}_H{h}_K", f"L{layer}_H{h}_V"]
+    x = torch.stack(sl).cuda()
+    analyze_slices(x[:2], names[:2])                             # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = analyze_slices(x, names)
+    torch.cuda.synchronize()
+    gpu_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for i in range(2):
+        analysis_oracle.analyze_tensor(sl[i], names[i])
+    cpu_s = (time.perf_counter() - t0) / 2 * len(sl)
+    print(json.dumps({"config": "pre-fit KV analysis", "seq_len": seq_len, "slices": len(sl),
+                      "gpu_s": round(gpu_s, 4), "cpu_oracle_s_extrapolated": round(cpu_s, 2),
+                      "cpu_threads": torch.get_num_threads(),
+                      "mean_lag1": round(sum(o["lag1_autocorrelation"] for o in out) / len(out), 4)}),
+          flush=True)
+
+
 def scan(lens, epochs):
     for n in lens:
         t0 = time.perf_counter()
@@ -106,7 +138,7 @@ def scan(lens, epochs):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", nargs="+", choices=["single", "wide", "scan", "svd"])
+    ap.add_argument("which", nargs="+", choices=["single", "wide", "scan", "svd", "analysis"])
     ap.add_argument("--epochs", type=int, default=2000)
     ap.add_argument("--scan-lens", default="512,1024,2048,4096")
     args = ap.parse_args()
@@ -117,6 +149,8 @@ def main():
         single(CONFIG_WIDE, 8192, args.epochs, "5 wide SIREN")
     if "svd" in args.which:
         svd_baseline(8192)
+    if "analysis" in args.which:
+        analysis(8192)
     if "scan" in args.which:
         scan([int(x) for x in args.scan_lens.split(",")], args.epochs)
 
