@@ -129,6 +129,14 @@ __device__ unsigned long long* g_stamps = nullptr;
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+// scratch stores of the row kernel (activations / gradients for the parameter
+// kernel and the backward): non-temporal, so ≈3 GB of once-written lines per
+// launch do not evict the weight planes the LDS-DMA staging re-reads from L2
+// (measured −5 % row-kernel time at W = 256 and 512)
+__device__ __forceinline__ void sst(float* p, float v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void sst4(float* p, f4 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+}
 
 __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -675,6 +683,8 @@ __device__ __forceinline__ void stage_vec(float* dst, const float* src, int n, i
 // bf16x3, 2.88 vs 2.70 ms fp32 for the 160-fit medium group.)
 template <int W> struct RowsCfg {
   static constexpr int NSPLIT = W >= 512 ? 2 : 1;
+  // (W = 256 at one wave per SIMD — no VGPR spills, 512 registers — measured
+  // 25 % slower: the second wave's MFMAs are what fill the epilogue gaps)
   static constexpr int WAVES_PER_SIMD = W >= 512 ? 1 : 2;
   static constexpr int NWAVES = 4;
   static constexpr int THREADS = 64 * NWAVES, ROWS = 16 * NWAVES;
@@ -803,7 +813,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
     }
     if (train) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) SHb[(16 * J + q) * 16] = hp[J][q];
+      for (int q = 0; q < 4; ++q) sst(SHb + (16 * J + q) * 16, hp[J][q]);
     }
   }
   if constexpr (X3) {
@@ -831,9 +841,9 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
         },
         [&](int J) {
           if (train) {
-            st4(SCi + J * 256, cs_pend);
+            sst4(SCi + J * 256, cs_pend);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) SHi[(16 * J + q) * 16] = ho[J % JP][q];
+            for (int q = 0; q < 4; ++q) sst(SHi + (16 * J + q) * 16, ho[J % JP][q]);
           }
         });
   }
@@ -863,7 +873,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
         if (yo) st4(yo + 16 * J, y_pend);          // lane holds ŷ[r][16J+4g+q]
         if (train) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) SGb[(16 * J + q) * 16] = y[J][q];
+          for (int q = 0; q < 4; ++q) sst(SGb + (16 * J + q) * 16, y[J][q]);
         }
       });
   STAMP(3);
@@ -881,7 +891,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
     float* SZl = SZb + (int64_t)layer * WN;
     return [&, SZl](int K) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) SZl[(16 * K + q) * 16] = ho[K % JP][q];
+      for (int q = 0; q < 4; ++q) sst(SZl + (16 * K + q) * 16, ho[K % JP][q]);
     };
   };
   auto cos_pre = [&](int layer) {
@@ -1072,7 +1082,9 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // bf16x3 form of dw_tile.  Each staged f4 (feature i/4, rows 4(i%4)..+3 of a
 // 16-row block) is split once, at the LDS store, into three bf16 planes
 // [3][TJ+TK features][kFx] (48-B feature stride: every ds_read_b128 lane
-// group covers a bank row once); a lane then reads its 8 rows of a feature
+// group covers a bank row once; the ds_write_b64 stores stay 2-way
+// conflicted — layouts that free both, e.g. 32-B features plus 16 B of pad
+// per 16, measured 8-10 % slower); a lane then reads its 8 rows of a feature
 // as one 16-B slice per plane, and each (x, y) sub-tile takes six
 // v_mfma_f32_32x32x16_bf16 per 16-row block (hi and correction accumulators)
 // instead of eight v_mfma_f32_32x32x2_f32.  Bias sums come from the fp32
