@@ -1102,7 +1102,8 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
                                            float* lds_f) {
   constexpr int NTH = 64 * NW, WK = NW / 2;
   constexpr int NA = TJ / 64, NB = TK / WK / 32;
-  constexpr int NF4 = (TJ + TK) * 4, NPT = (NF4 + NTH - 1) / NTH, NPA = TJ * 4 / NTH;
+  constexpr int NF4 = (TJ + TK) * 4, NPT = (NF4 + NTH - 1) / NTH;
+  constexpr int NA4 = TJ * 4, NPA = (NA4 + NTH - 1) / NTH;   // A's f4 / rounds holding A
   constexpr int PLX = (TJ + TK) * kFx, BUFX = 3 * PLX;
   static_assert(NA >= 1 && NB >= 1 && NPA >= 1, "tile too small for the wave grid");
   uint16_t* lds = reinterpret_cast<uint16_t*>(lds_f);
@@ -1120,7 +1121,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
       const int i = tid + NTH * m;
-      if (m < NPA)
+      if (NA4 % NTH == 0 ? m < NPA : i < NA4)   // wave-uniform (NA4 % 64 == 0)
         st[m] = ld4(Ab + rb * sA + i * 4);
       else if (NF4 % NTH == 0 || i < NF4)
         st[m] = ld4(Bb + rb * sB + (i - TJ * 4) * 4);
@@ -1142,7 +1143,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
         *reinterpret_cast<u2*>(d) = vh;
         *reinterpret_cast<u2*>(d + PLX) = vm;
         *reinterpret_cast<u2*>(d + 2 * PLX) = vl;
-        if (m < NPA && count) bpart[m] += (v[0] + v[1]) + (v[2] + v[3]);
+        if (m < NPA && i < NA4 && count) bpart[m] += (v[0] + v[1]) + (v[2] + v[3]);
       }
     }
   };
@@ -1186,6 +1187,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     for (int x = 0; x < NA; ++x)
 #pragma unroll
       for (int y = 0; y < NB; ++y) mfma32x3(av[x], bv[y], hi[x][y], lo[x][y]);
+    // (measured slower, each 7-14 %: one accumulator per sub-tile; product-major
+    // issue order across sub-tiles; operands loaded straight to registers
+    // without LDS; a conflict-free LDS layout — this order and staging stay)
     lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
     __syncthreads();
   };
@@ -1239,7 +1243,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
       float s = bpart[m];
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
-      if ((tid & 3) == 0) {
+      if ((tid & 3) == 0 && tid + NTH * m < NA4) {
         const int64_t idx = pb + j0 + ((tid + NTH * m) >> 2);
         if (G) {
           G[idx] = s;
@@ -1253,19 +1257,27 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   }
 }
 
-template <int W, int D> struct ParamsCfg {
-  static constexpr int T = W < 128 ? W : 128;          // hidden-layer tile (both dims)
-  static constexpr int NW = 4, THREADS = 64 * NW;      // 256-wide tiles measured slower (1 WG/CU)
+// Tiles: dW[j0:j0+T][k0:k0+TK] on 4 waves, two workgroups per CU.  (WIDE:
+// T × 256 tiles on 8 waves, one workgroup per CU, reads each dZ column block
+// once instead of W/128 times — a quarter less operand traffic — yet measured
+// 7 % slower at W = 256 and 512.)
+template <int W, int D, bool X3> struct ParamsCfg {
+  static constexpr bool WIDE = false;
+  static constexpr int T = W < 128 ? W : 128;          // hidden-layer tile rows (j)
+  static constexpr int TK = WIDE ? 256 : T;            // tile columns (k), hidden and final
+  static constexpr int NW = WIDE ? 8 : 4, THREADS = 64 * NW;
+  static constexpr int MINB = WIDE ? 1 : 2;            // workgroups per CU (launch bound)
   static constexpr int TD = D < T ? D : T;             // final-layer tile rows
-  static constexpr int NT = W / T;
-  static constexpr int TH = NT * NT, TF = (D / TD) * NT, T0 = W / (16 * NW);
+  static constexpr int NTJ = W / T, NTK = W / TK;
+  static constexpr int TH = NTJ * NTK, TF = (D / TD) * NTK, T0 = W / (16 * NW);
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
 template <int W, int D, bool X3>
-__global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(KArgs a) {
-  using C = ParamsCfg<W, D>;
-  constexpr int LDS_F = X3 ? 2 * 3 * (2 * C::T) * kFx / 2 : 2 * (2 * C::T) * kFs;
+__global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, D, X3>::MINB))
+    k_step_params(KArgs a) {
+  using C = ParamsCfg<W, D, X3>;
+  constexpr int LDS_F = X3 ? 2 * 3 * (C::T + C::TK) * kFx / 2 : 2 * (2 * C::T) * kFs;
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   int fit, t;
   const int nt = C::tiles(a.L_max);
@@ -1295,30 +1307,30 @@ __global__ void __launch_bounds__((ParamsCfg<W, D>::THREADS), 2) k_step_params(K
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
     if constexpr (X3)
-      dw_tile_x3<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W,
-                                    SH + (int64_t)(layer - 1) * WN, W, (u / C::NT) * C::T,
-                                    (u % C::NT) * C::T, rb0, nb, G, P, M, V, XS, pw,
-                                    pw + (int64_t)W * W, xs_mat(W, D, L, false, layer),
-                                    xs_mat(W, D, L, true, layer), W, (u % C::NT) == 0,
-                                    step_size, bc2s, lds);
+      dw_tile_x3<C::T, C::TK, C::NW>(a, SZ + (int64_t)layer * WN, W,
+                                     SH + (int64_t)(layer - 1) * WN, W, (u / C::NTK) * C::T,
+                                     (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
+                                     pw + (int64_t)W * W, xs_mat(W, D, L, false, layer),
+                                     xs_mat(W, D, L, true, layer), W, (u % C::NTK) == 0,
+                                     step_size, bc2s, lds);
     else
       dw_tile<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN,
-                                 W, (u / C::NT) * C::T, (u % C::NT) * C::T, rb0, nb, G, P, M, V,
+                                 W, (u / C::NTK) * C::T, (u % C::NTK) * C::T, rb0, nb, G, P, M, V,
                                  PT, pw, pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
-                                 (u % C::NT) == 0, step_size, bc2s, lds);
+                                 (u % C::NTK) == 0, step_size, bc2s, lds);
   } else if (t < L * C::TH + C::TF) {
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
     if constexpr (X3)
-      dw_tile_x3<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
-                                     (u % C::NT) * C::T, rb0, nb, G, P, M, V, XS, pw,
-                                     pw + (int64_t)W * D, xs_mat(W, D, L, false, L + 1),
-                                     xs_mat(W, D, L, true, L + 1), D, (u % C::NT) == 0,
-                                     step_size, bc2s, lds);
+      dw_tile_x3<C::TD, C::TK, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
+                                      (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
+                                      pw + (int64_t)W * D, xs_mat(W, D, L, false, L + 1),
+                                      xs_mat(W, D, L, true, L + 1), D, (u % C::NTK) == 0,
+                                      step_size, bc2s, lds);
     else
-      dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NT) * C::TD,
-                                  (u % C::NT) * C::T, rb0, nb, G, P, M, V, PT, pw,
-                                  pw + (int64_t)W * D, (int64_t)L * W * W, D, (u % C::NT) == 0,
+      dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
+                                  (u % C::NTK) * C::T, rb0, nb, G, P, M, V, PT, pw,
+                                  pw + (int64_t)W * D, (int64_t)L * W * W, D, (u % C::NTK) == 0,
                                   step_size, bc2s, lds);
   } else {
     // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0.  Lane = (feature
@@ -1561,8 +1573,8 @@ int launch_rows(const KArgs& a, hipStream_t st) {
 
 template <int W, int D, bool X3>
 int launch_params(const KArgs& a, hipStream_t st) {
-  const int grid = grid_for(a.n_fits, ParamsCfg<W, D>::tiles(a.L_max) * a.n_split);
-  hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D>::THREADS), 0,
+  const int grid = grid_for(a.n_fits, ParamsCfg<W, D, X3>::tiles(a.L_max) * a.n_split);
+  hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS), 0,
                      st, a);
   if (a.n_split > 1) {
     const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
