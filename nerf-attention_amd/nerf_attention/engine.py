@@ -245,6 +245,26 @@ class _Group:
         return outs
 
 
+GROUP_MAX = 40
+
+
+def _chunks(members: list, cap: int) -> list:
+    """Split `members` into ceil(len/cap) chunks whose sizes are multiples of
+    8 (the last one takes the remainder); cap <= 0 keeps one chunk."""
+    n = len(members)
+    k = -(-n // cap) if cap > 0 else 1
+    octets, rem = divmod(n, 8)
+    if k <= 1 or octets < k:
+        return [members]
+    sizes = [8 * (octets // k + (1 if j < octets % k else 0)) for j in range(k)]
+    sizes[-1] += rem
+    out, at = [], 0
+    for z in sizes:
+        out.append(members[at:at + z])
+        at += z
+    return out
+
+
 def plan_groups(specs: list, devices: list) -> list:
     """[(device, [spec indices])] — LPT over devices, then (W, d, seq_len)."""
     costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
@@ -255,9 +275,18 @@ def plan_groups(specs: list, devices: list) -> list:
         k = (devices[dev_of[i]], s.config.hidden_features, int(s.target.shape[1]),
              int(s.target.shape[0]))
         keys.setdefault(k, []).append(i)
+    # Large groups are split into chunks of <= GROUP_MAX fits, each with its
+    # own stream: one chunk's row kernel (MFMA/LDS-bound) then overlaps another
+    # chunk's parameter kernel (HBM-bound) instead of the two alternating on
+    # one stream.  Chunk sizes stay multiples of 8 so the XCD-aware block map
+    # keeps every XCD busy.  Measured on the 280-fit sweep: +5 % (160-fit group
+    # -> 4 x 40), with GPU_MAX_HW_QUEUES = 8 so the streams get their own queues.
+    cap = int(os.environ.get("NERFHIP_GROUP_MAX", str(GROUP_MAX)))
+    parts = []
+    for k, m in keys.items():
+        parts += [(k[0], c) for c in _chunks(m, cap)]
     # heaviest groups first: they are enqueued (and start) first
-    return sorted(((k[0], m) for k, m in keys.items()),
-                  key=lambda dm: -sum(costs[i] for i in dm[1]))
+    return sorted(parts, key=lambda dm: -sum(costs[i] for i in dm[1]))
 
 
 class FitJob:

@@ -21,6 +21,7 @@ so the reference's per-fit wall clock has no direct equivalent.
 from __future__ import annotations
 
 import argparse
+import os
 import json
 import time
 from pathlib import Path
@@ -231,6 +232,8 @@ def _print_summary(all_results: list[dict], layers_to_fit: list[int]) -> None:
 
 
 def main() -> None:
+    # one HIP hardware queue per group stream (before the runtime initialises)
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     parser = argparse.ArgumentParser(description='Fit SIRENs to KV cache')
     parser.add_argument('--kv_dir', type=str, default='results/kv_cache')
     parser.add_argument('--output_dir', type=str, default='results/fits')

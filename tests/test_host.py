@@ -194,3 +194,17 @@ def test_custom_ops_registered_with_fakes():
         assert params.shape == (2, P) and losses.shape == (2, 7) and rc.shape == (2, 96)
         y = torch.ops.nerfhip.siren_forward(init[0], torch.empty(96), 64, 1, 30.0, 64)
         assert y.shape == (96, 64)
+
+
+def test_plan_groups_chunks_large_groups():
+    """Groups above GROUP_MAX split into multiple-of-8 chunks (one stream each);
+    the sweep's 160-fit W=256 group becomes 4 x 40; small groups stay whole."""
+    from nerf_attention.workloads import sweep_280
+    _, specs = sweep_280(64, seed=0)
+    groups = engine.plan_groups(specs, [0])
+    sizes = sorted(len(m) for _, m in groups)
+    assert sizes == [40] * 7
+    assert sorted(i for _, m in groups for i in m) == list(range(280))
+    assert [len(c) for c in engine._chunks(list(range(100)), 40)] == [32, 32, 36]
+    assert [len(c) for c in engine._chunks(list(range(9)), 40)] == [9]
+    assert [len(c) for c in engine._chunks(list(range(160)), 0)] == [160]
