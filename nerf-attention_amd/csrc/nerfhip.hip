@@ -132,7 +132,8 @@ __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) 
 // scratch stores of the row kernel (activations / gradients for the parameter
 // kernel and the backward): non-temporal, so ≈3 GB of once-written lines per
 // launch do not evict the weight planes the LDS-DMA staging re-reads from L2
-// (measured −5 % row-kernel time at W = 256 and 512)
+// (measured −5 % row-kernel time at W = 256 and 512; non-temporal loads of the
+// scratch, in both kernels, measured 1.6 % slower on the sweep)
 __device__ __forceinline__ void sst(float* p, float v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ void sst4(float* p, f4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
@@ -910,15 +911,43 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
     wide_layer(ic<4>, ic<1>, wsrc(true, i), hb, cos_pre(i - 1), dz_out, dz_store(i - 1));
   // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op sequence
   stage_vec(bias, P, 2 * W, tid);   // visible after gemm_phase's prologue barrier
-  wide_layer(ic<4>, ic<0>, wsrc(true, 1), hb, no_pre,
-             [&](int K, int q, float acc, float) {
-               const int f = 16 * K + 4 * g + q;
-               const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
-               float s, co;
-               sincos_fast(__fmul_rn(om, z), &s, &co);
-               ho[K % JP][q] = __fmul_rn(__fmul_rn(acc, co), om);
-             },
-             dz_store(0));
+  auto dz0_out = [&](int K, int q, float acc, float) {
+    const int f = 16 * K + 4 * g + q;
+    const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
+    float s, co;
+    sincos_fast(__fmul_rn(om, z), &s, &co);
+    ho[K % JP][q] = __fmul_rn(__fmul_rn(acc, co), om);
+  };
+  // dZ0 is only ever reduced (dw0 = Σ_r dZ0[r]·x_r, db0 = Σ_r dZ0[r]), so the
+  // wave reduces its 16 rows here and stores 2W partial sums per 16-row block
+  // ([n_pad/16][2][W] in dZ0's scratch slot: 1/8 of the bytes) instead of
+  // dZ0 itself.  Reduce-scatter over the 16 lanes c of a lane group g: after
+  // the xor-8/4/2/1 steps lanes c, c^1 hold value 4·c3 + 2·c2 + c1 of
+  // {Σ dz·x for q = 0..3, Σ dz for q = 0..3}.
+  float* PZ = SZ + (int64_t)rblk * 2 * W;
+  auto dz0_reduce = [&, PZ](int K) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = __fmul_rn(ho[K % JP][q], x);
+      v[4 + q] = ho[K % JP][q];
+    }
+    const bool b8 = c & 8, b4 = c & 4, b2 = c & 2;
+    float w[4], y[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = (b8 ? v[i + 4] : v[i]) + __shfl_xor(b8 ? v[i] : v[i + 4], 8, 64);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      y[i] = (b4 ? w[i + 2] : w[i]) + __shfl_xor(b4 ? w[i] : w[i + 2], 4, 64);
+    float t = (b2 ? y[1] : y[0]) + __shfl_xor(b2 ? y[0] : y[1], 2, 64);
+    t += __shfl_xor(t, 1, 64);
+    if (!(c & 1)) {
+      const int idx = (c >> 1);                 // 4·c3 + 2·c2 + c1
+      sst(PZ + (idx >> 2) * W + 16 * K + 4 * g + (idx & 3), t);
+    }
+  };
+  wide_layer(ic<1>, ic<0>, wsrc(true, 1), hb, no_pre, dz0_out, dz0_reduce);
   STAMP(5);
 }
 
@@ -1334,18 +1363,18 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, 
                                   step_size, bc2s, lds);
   } else {
     // first SineLayer(1, W): dw0 = dZ0ᵀ·x, db0 = Σ_rows dZ0.  Lane = (feature
-    // f = lane/4 of the wave's 16, quarter m = lane%4 of a 16-row block).
+    // f = lane/4 of the wave's 16, m = lane%4: every 4th 16-row block).
     const int u = t - L * C::TH - C::TF;
     const int f = lane >> 2, m = lane & 3;
     const int j = u * (16 * C::NW) + wave * 16 + f;
-    const float* zp = SZ + (int64_t)j * 16 + 4 * m;
-    const float* xp = a.pos + 4 * m;
     float sw = 0.f, sb = 0.f;
+    // the row kernel left per-16-row-block partial sums [n_pad/16][2][W]
+    // (+0.6 % on the sweep over storing dZ0 and reducing it here)
+    const float* pz = SZ + j;
 #pragma unroll 4
-    for (int rb = rb0; rb < rb0 + nb; ++rb) {
-      const f4 z = ld4(zp + (int64_t)rb * W * 16), x = ld4(xp + rb * 16);
-      sw += (z[0] * x[0] + z[1] * x[1]) + (z[2] * x[2] + z[3] * x[3]);
-      sb += (z[0] + z[1]) + (z[2] + z[3]);
+    for (int rb = rb0 + m; rb < rb0 + nb; rb += 4) {
+      sw += pz[(int64_t)rb * 2 * W];
+      sb += pz[(int64_t)rb * 2 * W + W];
     }
     sw += __shfl_xor(sw, 1, 64);
     sw += __shfl_xor(sw, 2, 64);
