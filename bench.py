@@ -197,22 +197,28 @@ def main() -> None:
         value = n_total * args.steps / t_max
         roof = None
         if any(k[2] for k in kt):
-            # dominant kernel = largest summed device time over the timed steps
+            # dominant kernel = largest summed device time over the timed steps,
+            # summed over every group (chunk) of that width
             N = args.seq_len
-            cands = []
+            per_kernel = {}     # name -> [total ms, launches, total flops, heaviest group]
             for g, (r_ms, p_ms, n) in zip(job.groups, kt):
+                if n == 0:
+                    continue
                 cf = [specs[mine[i]].config for i in g.members]
-                cands.append((r_ms, f"k_step_rows<{g.W},128>", r_ms / n, rows_flops(N, 128, cf), g))
-                cands.append((p_ms, f"k_step_params<{g.W},128>", p_ms / n,
-                              params_flops(N, 128, cf), g))
-            # per kernel: total device ms / launches over every group of that width
-            per_kernel = {}
-            for tot, name, avg, _, _ in cands:
-                acc = per_kernel.setdefault(name, [0.0, 0.0])
-                acc[0] += tot
-                acc[1] += tot / avg if avg > 0 else 0.0
-            _, kname, avg_ms, flops, g = max(cands, key=lambda c: c[0])
-            achieved = flops / (avg_ms * 1e-3) / 1e12
+                for name, ms, fl in ((f"k_step_rows<{g.W},128>", r_ms, rows_flops(N, 128, cf)),
+                                     (f"k_step_params<{g.W},128>", p_ms,
+                                      params_flops(N, 128, cf))):
+                    acc = per_kernel.setdefault(name, [0.0, 0, 0.0, None, 0.0])
+                    acc[0] += ms
+                    acc[1] += n
+                    acc[2] += fl * n
+                    if ms > acc[4]:
+                        acc[3], acc[4] = g, ms
+            kname, (tot_ms, n_launch, tot_flops, g, _) = max(per_kernel.items(),
+                                                             key=lambda kv: kv[1][0])
+            avg_ms = tot_ms / n_launch
+            flops = tot_flops / n_launch
+            achieved = tot_flops / (tot_ms * 1e-3) / 1e12
             traffic = None
             if PMC_TRAFFIC.exists():
                 traffic = json.loads(PMC_TRAFFIC.read_text()).get(f"{kname}[{args.precision}]")
@@ -223,23 +229,29 @@ def main() -> None:
             roof = {"bound": "mfma", "achieved": round(achieved, 3),
                     "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                    "kernel": f"{kname} [{args.precision}]", "fits_per_launch": g.n,
+                    "kernel": f"{kname} [{args.precision}]",
+                    "fits_per_launch": round(sum(x.n for x in job.groups
+                                                 if f"<{x.W}," in kname) /
+                                             sum(1 for x in job.groups if f"<{x.W}," in kname),
+                                             2),
                     "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": flops,
                     "flops_unit": "algorithmic fp32 GEMM FLOPs (2 per multiply-add), "
                                   "SURVEY.md §8d",
                     "peak_basis": ("f32 MFMA" if args.precision == "fp32" else
                                    "bf16 MFMA 2.5 PF dense / 6 bf16 products per fp32 product"),
                     "note": "launch durations measured while the width groups run concurrently",
-                    "kernels_avg_ms": {k: round(v[0] / v[1], 4) for k, v in per_kernel.items()
-                                       if v[1] > 0},
+                    "kernels_avg_ms": {k: round(v[0] / v[1], 4) for k, v in per_kernel.items()},
                     "groups": len(job.groups),
                     "job_achieved_tflops": round(job_tf, 2),
                     "job_frac": round(job_tf / peak, 4),
                     "job_frac_of_f32_mfma_peak": round(job_tf / FP32_MFMA_PEAK_TFLOPS, 4)}
             if world == 1:
+                gcf = [specs[mine[i]].config for i in g.members]
+                g_flops = (rows_flops if "rows" in kname else params_flops)(N, 128, gcf)
                 roof["isolated"] = isolated_kernel(
-                    [specs[mine[i]] for i in g.members], kname, flops, args.precision, peak,
+                    [specs[mine[i]] for i in g.members], kname, g_flops, args.precision, peak,
                     local)
+                roof["isolated"]["fits"] = g.n
         parity = None
         if GOLDEN_SWEEP.exists() and args.epochs == 2000 and args.seq_len == 2048:
             ref = json.loads(GOLDEN_SWEEP.read_text())["records"]
