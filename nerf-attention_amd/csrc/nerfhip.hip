@@ -139,6 +139,33 @@ __device__ __forceinline__ void sst4(float* p, f4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
 }
 
+template <int CTRL> __device__ __forceinline__ float dpp_quad(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// 4×4 transpose inside lane quads (two DPP quad_perm exchange rounds, xor 1
+// then xor 2): lane b of a quad ends up with element b of every quad lane,
+// v[k] = (lane k's v[b]).  The row kernel's accumulator lane (row c, group g)
+// holds features 4g+q of one row; after the transpose lane 4a+b holds feature
+// 4g+b of rows 4a..4a+3, which are adjacent in the row-block-major scratch —
+// one 16-B store per lane writes a 16-feature × 16-row tile as one contiguous
+// 1 KB run (whole 128-B lines) instead of four dword stores of 64-B pieces.
+__device__ __forceinline__ f4 quad_transpose(f4 v, int c) {
+  const bool o1 = c & 1, o2 = c & 2;
+  float r0 = dpp_quad<0xB1>(o1 ? v[0] : v[1]), r1 = dpp_quad<0xB1>(o1 ? v[2] : v[3]);
+  v[0] = o1 ? r0 : v[0];
+  v[1] = o1 ? v[1] : r0;
+  v[2] = o1 ? r1 : v[2];
+  v[3] = o1 ? v[3] : r1;
+  r0 = dpp_quad<0x4E>(o2 ? v[0] : v[2]);
+  r1 = dpp_quad<0x4E>(o2 ? v[1] : v[3]);
+  v[0] = o2 ? r0 : v[0];
+  v[1] = o2 ? r1 : v[1];
+  v[2] = o2 ? v[2] : r0;
+  v[3] = o2 ? v[3] : r1;
+  return v;
+}
+
 __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -682,6 +709,12 @@ __device__ __forceinline__ void stage_vec(float* dst, const float* src, int n, i
 // Rows per workgroup: 16 per wave.  (8 waves = 128 rows per workgroup at W = 256
 // halves the weight staging per row but measured no faster: 1.98 vs 2.03 ms
 // bf16x3, 2.88 vs 2.70 ms fp32 for the 160-fit medium group.)
+#ifdef NERFHIP_EXP_DWORD_STORES
+constexpr bool kQuadStores = false;   // diagnostic: the pre-transpose dword stores
+#else
+constexpr bool kQuadStores = true;
+#endif
+
 template <int W> struct RowsCfg {
   static constexpr int NSPLIT = W >= 512 ? 2 : 1;
   // (W = 256 at one wave per SIMD — no VGPR spills, 512 registers — measured
@@ -732,6 +765,22 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   float* SHb = SH + (int64_t)rblk * W * 16 + g * 64 + c;
   float* SZb = SZ + (int64_t)rblk * W * 16 + g * 64 + c;
   float* SGb = SG + (int64_t)rblk * D * 16 + g * 64 + c;
+  // after quad_transpose the lane writes feature 4g+(c&3) of rows 4(c>>2)..+3
+  const int tq = g * 64 + (c & 3) * 16 + (c >> 2) * 4;
+  float* SHt = SH + (int64_t)rblk * W * 16 + tq;
+  float* SZt = SZ + (int64_t)rblk * W * 16 + tq;
+  float* SGt = SG + (int64_t)rblk * D * 16 + tq;
+  // one transposed 16-B store per accumulator tile (kQuadStores), or four dword stores
+  auto tile_store = [&](float* base_t, float* base_d, int J, const float (&v)[4]) {
+    if constexpr (kQuadStores) {
+      const f4 t = {v[0], v[1], v[2], v[3]};
+      sst4(base_t + J * 256, quad_transpose(t, c));
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sst(base_d + (16 * J + q) * 16, v[q]);
+    }
+  };
+  constexpr int kTS = kQuadStores ? 1 : 4;   // vm stores per tile_store
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   auto no_pre = [&](int) { return zero4; };
 
@@ -813,8 +862,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
       hp[J][q] = s;
     }
     if (train) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sst(SHb + (16 * J + q) * 16, hp[J][q]);
+      tile_store(SHt, SHb, J, hp[J]);
     }
   }
   if constexpr (X3) {
@@ -829,10 +877,11 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
     const float* Wi = P + off_hidden_w(W, i);
     stage_vec(bias, Wi + W * W, W, tid);
     float* SHi = SHb + (int64_t)i * WN;
+    float* SHti = SHt + (int64_t)i * WN;
     float* SCi = SC + (int64_t)i * WN + (int64_t)rblk * JW * 256 + lane * 4;
     f4 cs_pend;
     wide_layer(
-        ic<TRAIN ? 5 : 0>, ic<0>, wsrc(false, i), hb, no_pre,
+        ic<TRAIN ? 1 + kTS : 0>, ic<0>, wsrc(false, i), hb, no_pre,
         [&](int J, int q, float acc, float) {
           const float z = __fadd_rn(acc, bias[16 * J + 4 * g + q]);
           float s, co;
@@ -843,8 +892,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
         [&](int J) {
           if (train) {
             sst4(SCi + J * 256, cs_pend);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sst(SHi + (16 * J + q) * 16, ho[J % JP][q]);
+            tile_store(SHti, SHi, J, ho[J % JP]);
           }
         });
   }
@@ -859,7 +907,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   S8 ys[JD / 2];
   float sq = 0.f;
   f4 y_pend;
-  gemm_any<X3, W, JD, NTH, TRAIN ? 4 : 0, TRAIN ? 1 : 0>(
+  gemm_any<X3, W, JD, NTH, TRAIN ? kTS : 0, TRAIN ? 1 : 0>(
       wsrc(false, L + 1), lds, xring, hb, tid, c, g,
       [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
       [&](int J, int q, float acc, float t) {
@@ -872,10 +920,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
       },
       [&](int J) {
         if (yo) st4(yo + 16 * J, y_pend);          // lane holds ŷ[r][16J+4g+q]
-        if (train) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) sst(SGb + (16 * J + q) * 16, y[J][q]);
-        }
+        if (train) tile_store(SGt, SGb, J, y[J]);
       });
   STAMP(3);
   if (!train) return;
@@ -890,10 +935,8 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   };
   auto dz_store = [&](int layer) {
     float* SZl = SZb + (int64_t)layer * WN;
-    return [&, SZl](int K) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sst(SZl + (16 * K + q) * 16, ho[K % JP][q]);
-    };
+    float* SZtl = SZt + (int64_t)layer * WN;
+    return [&, SZl, SZtl](int K) { tile_store(SZtl, SZl, K, ho[K % JP]); };
   };
   auto cos_pre = [&](int layer) {
     const float* SCl = SC + (int64_t)layer * WN + (int64_t)rblk * JW * 256 + lane * 4;
@@ -904,11 +947,11 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
     for (int J2 = 0; J2 < JD / 2; ++J2) ys[J2] = split_pair(y[2 * J2], y[2 * J2 + 1]);
   }
   auto& yb = pick_ref<X3>(ys, y);
-  wide_layer(ic<4>, ic<1>, wsrc(true, L + 1), yb, cos_pre(L), dz_out,
+  wide_layer(ic<kTS>, ic<1>, wsrc(true, L + 1), yb, cos_pre(L), dz_out,
              dz_store(L));   // W_fᵀ [W][D]
   STAMP(4);
   for (int i = L; i >= 2; --i)
-    wide_layer(ic<4>, ic<1>, wsrc(true, i), hb, cos_pre(i - 1), dz_out, dz_store(i - 1));
+    wide_layer(ic<kTS>, ic<1>, wsrc(true, i), hb, cos_pre(i - 1), dz_out, dz_store(i - 1));
   // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op sequence
   stage_vec(bias, P, 2 * W, tid);   // visible after gemm_phase's prologue barrier
   auto dz0_out = [&](int K, int q, float acc, float) {
