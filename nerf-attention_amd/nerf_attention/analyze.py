@@ -59,12 +59,45 @@ def effective_rank(S: torch.Tensor, threshold: float = 0.99) -> dict:
     }
 
 
+ENGINE_MAX_SEQ = 8192   # nerfhip_kv_analysis keeps a column + twiddles in LDS
+
+
+def _host_measures(slices: torch.Tensor, dims, max_lag: int) -> dict:
+    """The same measures on the CPU with numpy, per column as analyze.py:20-44
+    defines them (explicit device='cpu' only, e.g. quickstart --cpu)."""
+    x = slices.detach().to('cpu', torch.float32).numpy()
+    T, N, _ = x.shape
+    ac = np.zeros((T, len(dims), max_lag + 1))
+    en = np.ones((T, len(dims), 4))
+    hann = np.hanning(N)
+    for t in range(T):
+        for i, d in enumerate(dims):
+            col = x[t, :, d]
+            c = col - col.mean()
+            var = (c ** 2).sum()
+            if var >= 1e-10:
+                for lag in range(min(max_lag + 1, N)):
+                    ac[t, i, lag] = (c[:N - lag] * c[lag:]).sum() / var
+            p = np.abs(np.fft.rfft((col - col.mean()) * hann)) ** 2
+            tot = p.sum()
+            if tot >= 1e-10:
+                en[t, i] = [p[:max(1, int(len(p) * f))].sum() / tot for f in (0.05, 0.10, 0.25, 0.50)]
+    return {"autocorr": ac, "energy": en}
+
+
 def kv_measures(slices: torch.Tensor, dims, max_lag: int = MAX_LAG) -> dict:
     """Autocorrelation [T, n_dims, max_lag+1] and spectral-energy fractions
-    [T, n_dims, 4] (top 5/10/25/50 %) of the given columns of every slice."""
+    [T, n_dims, 4] (top 5/10/25/50 %) of the given columns of every slice:
+    on the engine for a HIP tensor, with numpy for a CPU tensor."""
+    if slices.device.type == 'cpu':
+        return _host_measures(slices, [int(d) for d in dims], max_lag)
     dev = engine.resolve_device(slices.device)
     x = slices.detach().to(dev, torch.float32).contiguous()
     T, N, D = x.shape
+    if N > ENGINE_MAX_SEQ:
+        raise _native.NerfhipError(
+            f"KV analysis on the engine takes seq_len <= {ENGINE_MAX_SEQ} (got {N}); analyse "
+            "longer caches with device='cpu'")
     dims = [int(d) for d in dims]
     f64 = dict(dtype=torch.float64, device=dev)
     ac = torch.empty(T, len(dims), max_lag + 1, **f64)
@@ -84,7 +117,12 @@ def analyze_slices(slices: torch.Tensor, names: list) -> list[dict]:
     T, N, D = slices.shape
     dims = sampled_dims(D)
     m = kv_measures(slices, dims)
-    sigma = rank_metrics(slices, [1])["sigma"]          # fp64, descending
+    if slices.device.type == 'cpu':     # torch.linalg.svd's singular values (analyze.py:48)
+        sigma = torch.linalg.svdvals(slices.to(torch.float32)).double().numpy()
+    else:
+        # fp64, descending; the D x D Gram gives D values, the SVD of an N x D
+        # slice has min(N, D) (the rest are zero up to rounding)
+        sigma = rank_metrics(slices, [1])["sigma"][:, :min(N, D)]
     keys = ('top_5pct', 'top_10pct', 'top_25pct', 'top_50pct')
     out = []
     for t in range(T):
@@ -101,13 +139,19 @@ def analyze_slices(slices: torch.Tensor, names: list) -> list[dict]:
     return out
 
 
-def analyze_kv_cache(kv_dir: Path, output_dir: Path, device: str = 'cuda') -> AnalysisResult:
-    """analyze.py:95-213 on the engine (without the figure)."""
+def analyze_kv_cache(kv_dir: Path, output_dir: Path, device: str | None = None) -> AnalysisResult:
+    """analyze.py:95-213 on the engine (without the figure).  The reference's
+    signature has no device (it analyses on the CPU); here device=None means
+    the HIP device when there is one, else the CPU (the reference's own
+    computation, as quickstart --cpu needs); 'cuda' / 'cpu' force either."""
+    if device is None:
+        device = 'cuda' if torch.cuda.is_available() else 'cpu' 
     kv_dir, output_dir = Path(kv_dir), Path(output_dir)
     output_dir.mkdir(parents=True, exist_ok=True)
     with open(kv_dir / 'metadata.json') as f:
         metadata = KVMetadata.from_dict(json.load(f))
-    dev = engine.resolve_device(device)
+    dev = torch.device('cpu') if torch.device(device).type == 'cpu' else \
+        engine.resolve_device(device)
     print(f"Analyzing KV cache: {metadata.num_layers} layers x {metadata.num_kv_heads} heads")
     print(f"Sequence length: {metadata.seq_len}, Head dim: {metadata.head_dim}")
 
@@ -201,7 +245,7 @@ def main() -> None:
     ap = argparse.ArgumentParser(description='Analyze KV cache structure (MI355X engine)')
     ap.add_argument('--kv_dir', type=str, default='results/kv_cache')
     ap.add_argument('--output_dir', type=str, default='results/analysis')
-    ap.add_argument('--device', type=str, default='cuda')
+    ap.add_argument('--device', type=str, default=None)
     args = ap.parse_args()
     analyze_kv_cache(Path(args.kv_dir), Path(args.output_dir), args.device)
 

@@ -12,9 +12,10 @@ running its own 2000-iteration eager loop with a host sync per epoch
   differ inside a group: medium/deep/hifreq/lofreq share W = 256);
 * every group gets its own HIP stream and the C side interleaves the groups'
   launches epoch by epoch, so the groups run concurrently;
-* several devices can be driven from one process (`devices=[0, 1, ...]`),
-  fits assigned by longest-processing-time on the FLOP model of SURVEY §8d.
-  `bench.py` instead runs one process per GPU and passes `devices=[rank]`.
+* a FitJob lives on ONE device; several devices mean several processes
+  (`run_fits(devices=[0, 1, ...])` hands the fits to `farm.run_farm`, one
+  worker process per GPU with its longest-processing-time share on the FLOP
+  model of SURVEY §8d; `bench.py` runs one rank per GPU the same way).
 
 There is deliberately no CPU path: a non-CUDA device raises.
 """
@@ -54,7 +55,11 @@ class FitOutput:
     row_mse: np.ndarray           # [seq_len] final per-row MSE (siren.py:125)
     final_mse: float              # siren.py:123
     probes: list = field(default_factory=list)  # (epoch, norm_mse, real_mse, cos)
+    # the reference's quantity (siren.py:96,117): wall clock of the epoch loop
+    # that trained this fit — here its group's loop, shared by every fit of the
+    # group (they train concurrently, so the sum over fits overcounts)
     train_time_seconds: float = 0.0
+    flop_share_seconds: float = 0.0   # group time x this fit's share of its FLOPs
     group_seconds: float = 0.0
     device: int = 0
 
@@ -91,8 +96,9 @@ def resolve_device(device) -> torch.device:
     dev = torch.device(device)
     if dev.type != "cuda":
         raise _native.NerfhipError(
-            f"nerf-attention-amd trains on MI355X only (device={device!r}); there is no CPU "
-            "path. The reference CPU loop lives in oracle/ as a test checker.")
+            f"the MI355X engine needs a HIP device (device={device!r}); there is no CPU "
+            "fallback on the engine path (only fit_siren/fit_kv_cache take an explicit "
+            "device='cpu', host_fit.py)")
     if not torch.cuda.is_available():
         raise _native.NerfhipError("no HIP device visible (torch.cuda.is_available() is False)")
     return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
@@ -140,17 +146,22 @@ class _Group:
         dev = torch.device("cuda", device)
         f32 = dict(dtype=torch.float32, device=dev)
 
-        # host-side packing (once per fit: the reference's H2D copies, siren.py:82-89)
-        pos = torch.zeros(n_pad, dtype=torch.float32)
+        # packing (the reference's H2D copies, siren.py:82-89): on the host and
+        # one copy per buffer when the inputs are host tensors, directly on the
+        # device when the caller already holds them there (torch.ops.nerfhip)
+        on_dev = all(specs[i].target.device == dev and specs[i].init.device == dev
+                     for i in members)
+        pack = dict(dtype=torch.float32, device=dev if on_dev else "cpu")
+        pos = torch.zeros(n_pad, **pack)
         pos[:self.N] = torch.linspace(0, 1, self.N)
-        tgt = torch.zeros(n, n_pad, self.D, dtype=torch.float32)
-        prm = torch.zeros(n, int(s.params), dtype=torch.float32)
+        tgt = torch.zeros(n, n_pad, self.D, **pack)
+        prm = torch.zeros(n, int(s.params), **pack)
         for k, i in enumerate(members):
             sp = specs[i]
             if tuple(sp.target.shape) != (self.N, self.D):
                 raise ValueError("all fits of a group must share (seq_len, d_head)")
-            tgt[k, :self.N] = sp.target.detach().to("cpu", torch.float32)
-            p = sp.init.detach().to("cpu", torch.float32).reshape(-1)
+            tgt[k, :self.N] = sp.target.detach().to(tgt.device, torch.float32)
+            p = sp.init.detach().to(prm.device, torch.float32).reshape(-1)
             if p.numel() != sp.config.num_parameters(self.D):
                 raise ValueError(f"init has {p.numel()} params, expected "
                                  f"{sp.config.num_parameters(self.D)}")
@@ -242,7 +253,8 @@ class _Group:
                 target_std=std[k].view(1, D).clone(),
                 losses=[float(x) for x in losses[k]], row_cos=row_cos[k].copy(),
                 row_mse=row_mse[k].copy(), final_mse=float(final_mse[k]), probes=probes,
-                train_time_seconds=group_seconds * flops[k] / tot,
+                train_time_seconds=group_seconds,
+                flop_share_seconds=group_seconds * flops[k] / tot,
                 group_seconds=group_seconds, device=self.device))
         return outs
 
@@ -267,14 +279,14 @@ def _chunks(members: list, cap: int) -> list:
     return out
 
 
-def plan_groups(specs: list, devices: list) -> list:
-    """[(device, [spec indices])] — LPT over devices, then (W, d, seq_len)."""
+def plan_groups(specs: list, device: int) -> list:
+    """[(device, [spec indices])] — fits grouped by (W, d, seq_len), large
+    groups chunked."""
     costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
              for s in specs]
-    dev_of = lpt_partition(costs, len(devices)) if len(devices) > 1 else [0] * len(specs)
     keys = {}
     for i, s in enumerate(specs):
-        k = (devices[dev_of[i]], s.config.hidden_features, int(s.target.shape[1]),
+        k = (device, s.config.hidden_features, int(s.target.shape[1]),
              int(s.target.shape[0]))
         keys.setdefault(k, []).append(i)
     # Large groups are split into chunks of <= GROUP_MAX fits, each with its
@@ -304,10 +316,14 @@ class FitJob:
         self.precision = check_precision(precision)
         if devices is None:
             devices = [resolve_device("cuda").index]
-        self.devices = [resolve_device(torch.device("cuda", d)).index for d in devices]
+        if len(devices) != 1:
+            raise ValueError("a FitJob runs on one device; farm several with run_fits("
+                             "devices=[...]) / farm.run_farm (one process per GPU)")
+        self.device = resolve_device(torch.device("cuda", devices[0])).index
+        self.devices = [self.device]
         self.specs = specs
         self.epochs = epochs
-        self.plan = plan_groups(specs, self.devices)
+        self.plan = plan_groups(specs, self.device)
         self.groups = [_Group(m, specs, epochs, lr, log_every, d, split, self.precision)
                        for d, m in self.plan]
         G = len(self.groups)
@@ -359,13 +375,65 @@ class FitJob:
 def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
              devices=None, precision: str | None = None) -> list:
     """Train every FitSpec for `epochs` Adam steps; returns FitOutput per spec
-    (same order).  Blocks until the device work is done."""
+    (same order).  Blocks until the device work is done.  More than one device:
+    one worker process per device (farm.run_farm), outputs' params on the host."""
     if not specs:
         return []
-    job = FitJob(specs, epochs, lr, log_every, devices, precision=precision)
-    job.launch()
-    job.wait()
-    return job.outputs()
+    if devices is not None and len(devices) > 1:
+        from . import farm
+        return farm.run_farm(specs, epochs, list(devices), lr=lr, log_every=log_every,
+                             precision=precision)
+    dev = resolve_device(torch.device("cuda", devices[0]) if devices else "cuda").index
+    need = [fit_device_bytes(s, epochs, log_every, precision) for s in specs]
+    waves = plan_waves(need, memory_budget(dev))
+    outs = [None] * len(specs)
+    for wave in waves:
+        job = FitJob([specs[i] for i in wave], epochs, lr, log_every, [dev], precision=precision)
+        job.launch()
+        job.wait()
+        for i, o in zip(wave, job.outputs()):
+            outs[i] = o
+        del job
+    return outs
+
+
+def fit_device_bytes(spec: FitSpec, epochs: int, log_every: int = 0, precision=None) -> int:
+    """Device bytes one fit occupies in a group (nerfhip_group_sizes buffers)."""
+    N, D = int(spec.target.shape[0]), int(spec.target.shape[1])
+    c = spec.config
+    s = _native.group_sizes(c.hidden_features, D, N, c.hidden_layers, epochs)
+    n_probe = epochs // log_every if log_every > 0 else 0
+    floats = (3 * s.params + s.params_t + s.scratch + 3 * s.target + 2 * s.stats
+              + max(s.loss_partial, 1) + 2 * s.rows + s.grad_partial
+              + n_probe * (s.target + 2 * s.rows))
+    return 4 * int(floats) + (2 * int(s.wsplit) if check_precision(precision) == "bf16x3" else 0)
+
+
+def memory_budget(device: int) -> int:
+    """Bytes a FitJob may allocate at once: NERFHIP_MEM_BUDGET_GB, else 60 % of
+    the device's HBM (288 GB on an MI355X)."""
+    env = os.environ.get("NERFHIP_MEM_BUDGET_GB")
+    if env:
+        return int(float(env) * 2 ** 30)
+    return int(0.6 * torch.cuda.get_device_properties(device).total_memory)
+
+
+def plan_waves(need: list, budget: int) -> list:
+    """Consecutive runs of fit indices whose summed bytes stay within `budget`
+    (a fit larger than the budget runs alone).  One wave when everything fits:
+    the 280-fit sweep needs ~6.5 GB.  Waves keep spec order, so results and the
+    reference's init order are unaffected (the reference's sequential loop
+    runs the same selection in constant memory, fit.py:54-76)."""
+    waves, cur, used = [], [], 0
+    for i, b in enumerate(need):
+        if cur and used + b > budget:
+            waves.append(cur)
+            cur, used = [], 0
+        cur.append(i)
+        used += b
+    if cur:
+        waves.append(cur)
+    return waves
 
 
 class ForwardPlan:

@@ -13,9 +13,14 @@ and then ALL fits are trained together on the HIP engine (grouped by width,
 one stream per group, optionally over several GPUs).  The per-fit progress
 lines are printed afterwards, in the reference order.
 
-`train_time_seconds` is each fit's share of its group's device time
-(group time × fit FLOPs / group FLOPs): fits of a group train concurrently,
-so the reference's per-fit wall clock has no direct equivalent.
+`train_time_seconds` keeps the reference's meaning (siren.py:96,117): the
+wall clock of the epoch loop that trained the fit.  Fits of a group train
+concurrently in one loop, so they share that figure and its sum over fits
+overcounts the sweep (the sweep's wall clock is printed at the end).
+
+With `gpus=N` (or `--gpus N`) the fits are farmed over N GPUs, one worker
+process per GPU (farm.run_farm), the same one-process-per-GPU design as
+bench.py.
 """
 
 from __future__ import annotations
@@ -76,6 +81,35 @@ def sweep_plan(layers, heads, configs, load_layer):
     return plan, skipped
 
 
+def _host_plan(plan, epochs: int, log_every: int):
+    """device='cpu' (BASELINE config 1): the fits one after the other in eager
+    PyTorch, each model initialised right before its fit as the reference
+    does (fit.py:70-76)."""
+    from .host_fit import fit_on_host
+    out = []
+    for _name, _l, _h, _kv, cfg, tensor in plan:
+        m = SIREN(cfg, out_features=int(tensor.shape[1]))
+        probes = []
+        res = fit_on_host(tensor, cfg, m, epochs, 1e-4, log_every,
+                          lambda *probe: probes.append(probe))
+        out.append((res, probes))
+    return out
+
+
+def _devices(device, gpus) -> list:
+    """Device indices to train on.  One GPU: the requested device.  Several:
+    one farm worker process per GPU (farm.run_farm); counted without
+    initialising HIP in this process (the workers are started first)."""
+    if not gpus or gpus <= 1:
+        return [engine.resolve_device(device).index]
+    if torch.device(device).type != 'cuda':
+        return [engine.resolve_device(device).index]     # raises: no CPU path
+    have = torch.cuda.device_count()
+    if have < gpus:
+        raise engine._native.NerfhipError(f"--gpus {gpus} but only {have} HIP device(s) visible")
+    return list(range(gpus))
+
+
 def train_plan(plan, epochs: int, devices, log_every: int, precision=None):
     """Initialise every model in plan order (the reference's RNG order), then
     train them all on the engine.  Returns [(FitResult, probes)]."""
@@ -122,8 +156,8 @@ def fit_kv_cache(
           f"{metadata.seq_len * metadata.head_dim * 2 / 1024:.1f} KB (float16 baseline)")
     print(f"Device: {device}, Epochs: {epochs}")
 
-    dev = engine.resolve_device(device)
-    devices = [dev.index] if not gpus or gpus <= 1 else list(range(gpus))
+    host = torch.device(device).type == 'cpu'
+    devices = None if host else _devices(device, gpus)
     layers, heads, configs = select_fits(metadata, quick, select, configs)
     total = len(layers) * heads * 2 * len(configs)
 
@@ -134,8 +168,9 @@ def fit_kv_cache(
         return torch.load(p, map_location='cpu', weights_only=True)
 
     plan, skipped = sweep_plan(layers, heads, configs, load_layer)
-    results = train_plan(plan, epochs, devices, log_every=max(epochs // 5, 100),
-                         precision=precision)
+    log_every = max(epochs // 5, 100)
+    results = _host_plan(plan, epochs, log_every) if host else \
+        train_plan(plan, epochs, devices, log_every=log_every, precision=precision)
 
     all_results: list[dict] = []
     count = 0

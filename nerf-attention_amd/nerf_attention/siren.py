@@ -12,7 +12,9 @@ parameters as the reference.
 `fit_siren` (siren.py:70-149) keeps the reference signature and returns the
 same `FitResult`, but the 2000-epoch loop runs on the HIP engine: two fused
 kernels per epoch, no per-epoch host sync, metrics computed on the device.
-There is no CPU fallback: device='cpu' raises.
+There is no CPU fallback: a HIP request without a HIP device raises.  Only an
+explicit device='cpu' (BASELINE config 1, `quickstart --cpu`) trains on the
+host, in eager PyTorch (host_fit.py).
 """
 
 from __future__ import annotations
@@ -67,13 +69,22 @@ class SIREN(nn.Module):
         self.out_features = out_features
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        # Inference on a CUDA device goes through the HIP forward kernel; with
-        # autograd recording (training through this module) or on the CPU the
-        # module is plain torch, as a CPU nn.Module must be.
-        if x.is_cuda and not (torch.is_grad_enabled() and
-                              any(p.requires_grad for p in self.parameters())):
+        # Inference on a HIP device goes through the HIP forward kernel.  With
+        # autograd recording (gradients wanted w.r.t. the parameters or the
+        # positions x), on the CPU, or for a shape the engine does not take
+        # (fewer than 2 positions, W/d_head/L outside the compiled set) the
+        # module is plain torch, as the nn.Module it is.
+        if x.is_cuda and self._engine_shape(x) and not (
+                torch.is_grad_enabled() and
+                (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
             return self._native_forward(x)
         return self.network(x)
+
+    def _engine_shape(self, x: torch.Tensor) -> bool:
+        c = self.siren_config
+        return (x.numel() >= 2 and (x.dim() == 1 or x.shape[-1] == 1)
+                and c.hidden_features in (64, 128, 256, 512)
+                and self.out_features in (64, 128) and 1 <= c.hidden_layers <= 4)
 
     def _native_forward(self, x: torch.Tensor) -> torch.Tensor:
         # The plan (device buffers + C-ABI descriptor) is cached across calls:
@@ -174,6 +185,13 @@ def fit_siren(
     picks the GEMM arithmetic — both meet the same per-fit parity bar.
     """
     seq_len, d_head = kv_tensor.shape
+    if torch.device(device).type == 'cpu':
+        # explicit host request (BASELINE config 1, quickstart --cpu): the
+        # eager PyTorch loop, see host_fit.py.  Never reached for 'cuda'.
+        from .host_fit import fit_on_host
+        model = SIREN(config, out_features=d_head)
+        show = (lambda e, n, r, c: print(probe_line(e, epochs, n, r, c))) if verbose else None
+        return fit_on_host(kv_tensor, config, model, epochs, lr, log_every, show)
     dev = engine.resolve_device(device)
     model = SIREN(config, out_features=d_head)
     spec = engine.FitSpec(target=kv_tensor, config=config, init=model.flat_parameters())

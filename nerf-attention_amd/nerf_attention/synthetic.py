@@ -16,62 +16,129 @@ single slice without generating the rest (the sweep needs 20 of 256).
 from __future__ import annotations
 
 import json
+import os
 from pathlib import Path
 
 import numpy as np
 import torch
 
+from ._synth_core import pool_job, slice_np
 from .types import KVMetadata
-
-
-def _sharpness(layer: int, num_layers: int) -> float:
-    return 1.0 + 2.0 * (layer / max(num_layers - 1, 1))        # extract.py:204
-
-
-def _spike_train(rng, seq_len: int, sharp: float) -> np.ndarray:
-    """Sparse Gaussian bumps, narrower and more numerous in deeper layers
-    (extract.py:219-228)."""
-    out = np.zeros(seq_len)
-    for _ in range(int(3 * sharp)):
-        centre = rng.randint(0, seq_len)
-        width = rng.randint(1, max(2, int(5 / sharp)))
-        amp = rng.uniform(0.5, 2.0)
-        for off in range(-width, width + 1):
-            at = centre + off
-            if 0 <= at < seq_len:
-                out[at] += amp * np.exp(-0.5 * (off / max(1, width / 2)) ** 2)
-    return out
 
 
 def kv_slice(layer: int, head: int, seq_len: int = 2048, num_layers: int = 32,
              num_kv_heads: int = 8, head_dim: int = 128):
     """(keys[seq_len, head_dim], values[seq_len, head_dim]) of one (layer, head)."""
-    rng = np.random.RandomState(layer * num_kv_heads + head)
     tt = torch.linspace(0, 1, seq_len).numpy()
-    sharp = _sharpness(layer, num_layers)
-    keys = np.empty((seq_len, head_dim), dtype=np.float32)
-    vals = np.empty((seq_len, head_dim), dtype=np.float32)
-    for j in range(head_dim):
-        f_lo, f_hi = rng.uniform(1, 5), rng.uniform(3, 10)
-        smooth = (0.5 * np.sin(2 * np.pi * f_lo * tt) +
-                  0.3 * np.cos(2 * np.pi * f_hi * tt))
-        f_mid = rng.uniform(10, 30)
-        ripple = 0.2 * np.sin(2 * np.pi * f_mid * tt + rng.uniform(0, 2 * np.pi))
-        bumps = _spike_train(rng, seq_len, sharp)
-        noise = rng.randn(seq_len) * 0.1
-        keys[:, j] = smooth + ripple + bumps + noise
-        v_wave = 0.6 * np.sin(2 * np.pi * rng.uniform(1, 8) * tt)
-        vals[:, j] = v_wave + rng.randn(seq_len) * 0.15
+    keys = np.empty((seq_len, head_dim), np.float32)
+    vals = np.empty((seq_len, head_dim), np.float32)
+    slice_np(tt, layer, head, num_layers, num_kv_heads, head_dim, keys, vals)
     return torch.from_numpy(keys), torch.from_numpy(vals)
+
+
+def _threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+POOL_MIN_ROWS = 32 * 4096     # slices x seq_len below which one process is faster
+
+
+def kv_slices(pairs, seq_len: int = 2048, num_layers: int = 32, num_kv_heads: int = 8,
+              head_dim: int = 128) -> list:
+    """kv_slice for every (layer, head) in `pairs`.  Large requests run on a
+    pool of fresh worker processes (the RandomState draws are a sequential
+    Python loop per slice, so threads serialise on the GIL): every slice has
+    its own RandomState, so the bits do not depend on the split; the workers
+    write into one shared-memory buffer."""
+    pairs = list(pairs)
+    workers = min(_threads(), len(pairs))
+    if workers <= 1 or len(pairs) * seq_len < POOL_MIN_ROWS:
+        return [kv_slice(l, h, seq_len, num_layers, num_kv_heads, head_dim) for l, h in pairs]
+    import mmap
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    from . import _synth_core
+    tt = torch.linspace(0, 1, seq_len).numpy()
+    shape = (len(pairs), 2, seq_len, head_dim)
+    nbytes = int(np.prod(shape)) * 4
+    jobs = [(k, l, h) for k, (l, h) in enumerate(pairs)]
+    parts = [jobs[w::workers] for w in range(workers)]
+    if not torch.cuda.is_initialized():
+        # fork: the workers inherit an anonymous shared mapping and write the
+        # slices straight into it; the result is a view of it (no copy)
+        mm = mmap.mmap(-1, nbytes, flags=mmap.MAP_SHARED)
+        _synth_core._SHARED = mm
+        try:
+            with ProcessPoolExecutor(max_workers=workers,
+                                     mp_context=mp.get_context("fork")) as ex:
+                for f in [ex.submit(_synth_core.pool_job_fork, shape, tt, part, num_layers,
+                                    num_kv_heads) for part in parts]:
+                    f.result()
+        finally:
+            _synth_core._SHARED = None
+        out = torch.from_numpy(np.frombuffer(mm, dtype=np.float32).reshape(shape))
+    else:
+        # this process has HIP state: fresh interpreters and a named segment
+        from multiprocessing import shared_memory
+        shm = shared_memory.SharedMemory(create=True, size=nbytes)
+        try:
+            with ProcessPoolExecutor(max_workers=workers,
+                                     mp_context=mp.get_context("spawn")) as ex:
+                for f in [ex.submit(pool_job, shm.name, shape, tt, part, num_layers,
+                                    num_kv_heads) for part in parts]:
+                    f.result()
+            buf = np.ndarray(shape, dtype=np.float32, buffer=shm.buf)
+            out = torch.from_numpy(buf.copy())
+            del buf
+        finally:
+            shm.close()
+            shm.unlink()
+    return [(out[k, 0], out[k, 1]) for k in range(len(pairs))]
 
 
 def kv_layer(layer: int, seq_len: int = 2048, num_layers: int = 32, num_kv_heads: int = 8,
              head_dim: int = 128, heads=None):
     """{'keys': [H', N, d], 'values': [H', N, d]} for heads (default: all)."""
     heads = range(num_kv_heads) if heads is None else heads
-    ks, vs = zip(*(kv_slice(layer, h, seq_len, num_layers, num_kv_heads, head_dim)
-                   for h in heads))
+    ks, vs = zip(*kv_slices([(layer, h) for h in heads], seq_len, num_layers, num_kv_heads,
+                            head_dim))
     return {'keys': torch.stack(ks), 'values': torch.stack(vs)}
+
+
+def kv_cache(layers, seq_len: int = 2048, num_layers: int = 32, num_kv_heads: int = 8,
+             head_dim: int = 128, heads=None) -> dict:
+    """{layer: kv_layer(layer)} for several layers, all slices generated on
+    one thread pool (BASELINE config 4 needs 32 x 8 of them per seq_len)."""
+    layers = list(layers)
+    heads = list(range(num_kv_heads) if heads is None else heads)
+    flat = kv_slices([(l, h) for l in layers for h in heads], seq_len, num_layers,
+                     num_kv_heads, head_dim)
+    out, k = {}, 0
+    for l in layers:
+        ks, vs = zip(*flat[k:k + len(heads)])
+        out[l] = {'keys': torch.stack(ks), 'values': torch.stack(vs)}
+        k += len(heads)
+    return out
+
+
+def write_kv_cache(output_dir: Path, seq_len: int = 2048, num_layers: int = 32,
+                   num_kv_heads: int = 8, head_dim: int = 128, layers=None) -> KVMetadata:
+    """The on-disk cache format (layer_XX.pt + metadata.json, extract.py:
+    238-259) for `layers` only (default all), without the progress lines."""
+    output_dir = Path(output_dir)
+    output_dir.mkdir(parents=True, exist_ok=True)
+    layers = range(num_layers) if layers is None else layers
+    for layer, data in kv_cache(layers, seq_len, num_layers, num_kv_heads, head_dim).items():
+        torch.save(data, output_dir / f'layer_{layer:02d}.pt')
+    meta = KVMetadata(model_name='synthetic', num_layers=num_layers, num_kv_heads=num_kv_heads,
+                      seq_len=seq_len, head_dim=head_dim, actual_tokens=seq_len)
+    with open(output_dir / 'metadata.json', 'w') as f:
+        json.dump(meta.to_dict(), f, indent=2)
+    return meta
 
 
 def extract_kv_cache_synthetic(
@@ -84,15 +151,7 @@ def extract_kv_cache_synthetic(
     """Write layer_XX.pt + metadata.json exactly as extract.py:182-259 does."""
     print("Generating synthetic KV cache...")
     print(f"  {num_layers} layers, {num_kv_heads} heads, seq_len={seq_len}, head_dim={head_dim}")
-    output_dir = Path(output_dir)
-    output_dir.mkdir(parents=True, exist_ok=True)
-    for layer in range(num_layers):
-        torch.save(kv_layer(layer, seq_len, num_layers, num_kv_heads, head_dim),
-                   output_dir / f'layer_{layer:02d}.pt')
-    meta = KVMetadata(model_name='synthetic', num_layers=num_layers, num_kv_heads=num_kv_heads,
-                      seq_len=seq_len, head_dim=head_dim, actual_tokens=seq_len)
-    with open(output_dir / 'metadata.json', 'w') as f:
-        json.dump(meta.to_dict(), f, indent=2)
+    meta = write_kv_cache(output_dir, seq_len, num_layers, num_kv_heads, head_dim)
     total_mb = num_layers * num_kv_heads * seq_len * head_dim * 2 * 4 / 1024 / 1024
     print(f"Saved to {output_dir}/ ({total_mb:.1f} MB)")
     return meta

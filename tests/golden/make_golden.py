@@ -186,6 +186,43 @@ def make_wide():
     (HERE / "wide_8192_e30.json").write_text(json.dumps(out, indent=1))
 
 
+SCAN_LENGTHS = (512, 1024, 4096)
+
+
+def make_scan():
+    """BASELINE config 4 seq-len points: medium fits of layers {0, L/2, L-1},
+    head 0, K and V at each length, exactly the selection of the reference's
+    scaling experiment (experiments/scaling.py:160-168), on the reference's
+    synthetic 32x8xNx128 cache.  torch.manual_seed(0) before every fit."""
+    siren, types, extract, _ = _ref()
+    medium = types.SIRENConfig(256, 2, 30.0, "medium")
+    out = {}
+    for n in SCAN_LENGTHS:
+        d = SCRATCH / f"kv_{n}"
+        if not (d / "layer_31.pt").exists():
+            with contextlib.redirect_stdout(io.StringIO()):
+                extract.extract_kv_cache_synthetic(seq_len=n, num_layers=32, num_kv_heads=8,
+                                                   head_dim=128, output_dir=d)
+        recs = []
+        for layer in (0, 16, 31):
+            data = torch.load(d / f"layer_{layer:02d}.pt", weights_only=True)
+            for kv, t in (("key", data["keys"][0]), ("value", data["values"][0])):
+                torch.manual_seed(0)
+                t0 = time.time()
+                r = siren.fit_siren(t, medium, epochs=2000, device="cpu", log_every=2000,
+                                    verbose=False)
+                recs.append({"name": f"L{layer}_H0_{kv}_medium", "layer": layer, "kv_type": kv,
+                             "target_sha256": sha(t.numpy()),
+                             "final_cosine_mean": r.final_cosine_mean,
+                             "final_cosine_min": r.final_cosine_min,
+                             "final_mse": r.final_mse, "losses_every100": r.losses[::100],
+                             "train_time_seconds_cpu": time.time() - t0})
+                print(n, recs[-1]["name"], r.final_cosine_mean, flush=True)
+        out[str(n)] = {"records": recs, "threads": torch.get_num_threads(),
+                       "torch": torch.__version__, "epochs": 2000, "seed": 0}
+    (HERE / "scan_medium_e2000.json").write_text(json.dumps(out, indent=1))
+
+
 def make_schema():
     _, _, _, fit = _ref()
     out = SCRATCH / "fits_quick_e20"

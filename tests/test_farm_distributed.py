@@ -71,3 +71,58 @@ def test_single_process_share_is_everything():
     assert farm.rank_share([3.0, 1.0, 2.0], 1, 0) == [0, 1, 2]
     assert farm.max_over_ranks(2.5) == 2.5
     assert farm.gather_records({1: "a"}) == {1: "a"}
+
+
+# ---- bench.py launcher (world 2 on CPU, gloo; no device work) -------------
+
+import json as _json
+import subprocess as _sp
+import sys as _sys
+from pathlib import Path as _Path
+
+_BENCH = _Path(__file__).resolve().parent.parent / "bench.py"
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(extra)
+    return env
+
+
+def test_bench_spawns_ranks_for_gpus_2():
+    """`python bench.py --gpus 2` without a launcher starts two ranks itself;
+    they form a gloo group, split the 280 fits by LPT and meet in the barrier,
+    max and gather; rank 0 prints one line that saw both ranks."""
+    r = _sp.run([_sys.executable, str(_BENCH), "--gpus", "2", "--dry-run"], env=_bench_env(),
+                capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = _json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
+    assert line["fits"] == list(range(280)) and set(line["owner"]) == {0, 1}
+    costs = _costs()
+    assert [farm.rank_share(costs, 2, k) for k in (0, 1)] == \
+        [[i for i, o in enumerate(line["owner"]) if o == k] for k in (0, 1)]
+    lo, hi = sorted(line["rank_flops"])
+    assert hi / lo < 1.05
+
+
+def test_bench_rejects_world_mismatch():
+    """A launcher world that disagrees with --gpus is an error, not a silent
+    single-GPU run."""
+    r = _sp.run([_sys.executable, str(_BENCH), "--gpus", "2", "--dry-run"],
+                env=_bench_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"),
+                capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_spawn_ranks_propagates_failure(tmp_path):
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "sys.exit(3) if r == 1 else time.sleep(30)\n")
+    t0 = __import__("time").time()
+    rc = farm.spawn_ranks(2, [], str(script))
+    assert rc == 3 and __import__("time").time() - t0 < 20   # rank 0 was terminated

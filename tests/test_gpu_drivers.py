@@ -1,0 +1,205 @@
+"""The drop-in drivers and the BASELINE configs end to end on the MI355X,
+against results of the reference itself (tests/golden/make_golden.py):
+
+* config 3, the 280-fit sweep at seq 2048 / 2000 epochs, every fit against
+  the reference's own seed-0 sweep (sweep_ref_seed0_e2000.json);
+* the per-rank shares of a 2- and an 8-GPU farm (smaller groups: the split-K
+  gradient path) trained alone, against the same golden;
+* config 4's seq-len points 512 / 1024 / 4096: the medium fits the
+  reference's scaling experiment runs per length (scan_medium_e2000.json);
+* `fit_kv_cache(quick=True)` and `python -m nerf_attention.fit --quick`
+  against the reference's own quick run (schema_quick/: records, key order,
+  checkpoint layout, stdout structure);
+* the one-process-per-GPU farm (two workers) equal to one process, bitwise.
+
+Tolerance: north_star's ±1e-3 on every fit's final cosine.  All GPU work goes
+through the C ABI (libnerfhip.so).
+"""
+
+import json
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from nerf_attention import SIREN, SIRENConfig, engine, farm
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-3
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _cos(o):
+    return float(torch.from_numpy(o.row_cos).mean())
+
+
+@pytest.fixture(scope="module")
+def sweep():
+    from nerf_attention.workloads import sweep_280
+    plan, specs = sweep_280(2048, seed=0)
+    return plan, specs
+
+
+def _ref_sweep(golden_dir):
+    recs = json.loads((golden_dir / "sweep_ref_seed0_e2000.json").read_text())["records"]
+    return {r["name"]: r for r in recs}
+
+
+def test_sweep_280_vs_reference(gpu, golden_dir, sweep):
+    """BASELINE config 3 on one GPU: all 280 fits within 1e-3 of the reference."""
+    plan, specs = sweep
+    ref = _ref_sweep(golden_dir)
+    outs = engine.run_fits(specs, 2000, devices=[0])
+    d = np.array([abs(_cos(o) - ref[p[0]]["final_cosine_mean"]) for p, o in zip(plan, outs)])
+    assert d.size == 280 and d.max() <= COS_TOL, (d.max(), plan[int(d.argmax())][0])
+    mse = np.array([o.final_mse / ref[p[0]]["final_mse"] for p, o in zip(plan, outs)])
+    assert np.abs(mse - 1).max() <= 0.05
+
+
+@pytest.mark.parametrize("world,rank", [(8, 0), (2, 1)])
+def test_rank_share_vs_reference(gpu, golden_dir, sweep, world, rank):
+    """What one rank of a `world`-GPU farm trains, alone on one GPU: its
+    groups are smaller (at 8 ranks the W = 512, 128 and 64 groups hold 5 fits
+    each, so their weight gradients take the split-K path), yet every fit
+    stays within 1e-3."""
+    plan, specs = sweep
+    ref = _ref_sweep(golden_dir)
+    costs = [engine.fit_flops(2048, 128, s.config, 2000) for s in specs]
+    mine = farm.rank_share(costs, world, rank)
+    outs = engine.run_fits([specs[i] for i in mine], 2000, devices=[0])
+    d = np.array([abs(_cos(o) - ref[plan[i][0]]["final_cosine_mean"]) for i, o in zip(mine, outs)])
+    assert d.max() <= COS_TOL, (d.max(), plan[mine[int(d.argmax())]][0])
+    if world == 8:
+        job = engine.FitJob([specs[i] for i in mine], 1, devices=[0])
+        split = {g.W for g in job.groups if g.grad_partial is not None}
+        assert split == {512, 128, 64}                 # the split-K path ran
+
+
+@pytest.mark.parametrize("seq_len", [512, 1024, 4096])
+def test_scan_points_vs_reference(gpu, golden_dir, seq_len):
+    """BASELINE config 4's seq-len points: medium fits of layers {0, 16, 31},
+    head 0, K and V (experiments/scaling.py:160-168) against the reference."""
+    from nerf_attention.synthetic import kv_slice
+    g = json.loads((golden_dir / "scan_medium_e2000.json").read_text())[str(seq_len)]
+    cfg = SIRENConfig(256, 2, 30.0, "medium")
+    torch.manual_seed(0)
+    init = SIREN(cfg, 128).flat_parameters()
+    specs = []
+    for r in g["records"]:
+        k, v = kv_slice(r["layer"], 0, seq_len=seq_len)
+        specs.append(engine.FitSpec(target=k if r["kv_type"] == "key" else v, config=cfg,
+                                    init=init))
+    outs = engine.run_fits(specs, 2000, devices=[0])
+    for r, o in zip(g["records"], outs):
+        assert abs(_cos(o) - r["final_cosine_mean"]) <= COS_TOL, (r["name"], _cos(o))
+        np.testing.assert_allclose(o.losses[::100][:5], r["losses_every100"][:5], rtol=1e-3)
+
+
+def _quick_cache(tmp):
+    from nerf_attention.synthetic import extract_kv_cache_synthetic
+    kv = Path(tmp) / "kv"
+    extract_kv_cache_synthetic(seq_len=512, num_layers=4, num_kv_heads=4, head_dim=128,
+                               output_dir=kv)
+    return kv
+
+
+_NUM = re.compile(r"-?\d+\.\d+")
+
+
+def _shape(text: str) -> list:
+    """stdout line structure: numbers masked, the device name normalised."""
+    return [_NUM.sub("#", l).replace("Device: cuda", "Device: cpu") for l in text.splitlines()]
+
+
+def _check_quick_outputs(golden_dir, recs, out_dir):
+    ref = json.loads((golden_dir / "schema_quick" / "fit_results.json").read_text())
+    layout = json.loads((golden_dir / "schema_quick" / "checkpoint_layout.json").read_text())
+    assert [list(r) for r in recs] == [list(r) for r in ref]              # names + key order
+    ints = ("layer", "head", "hidden_features", "hidden_layers", "raw_size_bytes",
+            "siren_size_bytes", "num_parameters", "seq_len", "d_head")
+    for a, b in zip(recs, ref):
+        assert all(a[k] == b[k] for k in ints + ("name", "kv_type", "config_name", "omega_0"))
+        assert abs(a["final_cosine_mean"] - b["final_cosine_mean"]) <= COS_TOL, a["name"]
+        assert a["compression_ratio"] == pytest.approx(b["compression_ratio"])
+    saved = json.loads((out_dir / "fit_results.json").read_text())
+    assert saved == json.loads(json.dumps(recs))
+    cks = sorted(out_dir.glob("*_model.pt"))
+    assert len(cks) == 6
+    ck = torch.load(out_dir / "L0_H0_key_medium_model.pt", weights_only=True)
+    assert list(ck) == layout["top_keys"]
+    assert list(ck["model_state"]) == layout["model_state_keys"]
+    assert {k: list(v.shape) for k, v in ck["model_state"].items()} == \
+        layout["model_state_shapes"]
+    assert ck["config"] == layout["config"]
+    assert list(ck["metrics"]) == layout["metrics_keys"]
+
+
+def test_fit_kv_cache_quick_vs_reference(gpu, golden_dir, tmp_path, capsys):
+    """fit_kv_cache(quick=True) end to end on the GPU — the drop-in driver
+    (fit.py:20-92) against the reference's own quick run."""
+    from nerf_attention import fit_kv_cache
+    kv = _quick_cache(tmp_path)
+    capsys.readouterr()
+    torch.manual_seed(0)
+    recs = fit_kv_cache(kv, tmp_path / "fits", epochs=20, device="cuda", quick=True)
+    out = capsys.readouterr().out
+    _check_quick_outputs(golden_dir, recs, tmp_path / "fits")
+    ref_out = (golden_dir / "schema_quick" / "stdout.txt").read_text()
+    assert _shape(out) == _shape(ref_out)
+
+
+def test_fit_cli_quick(gpu, golden_dir, tmp_path):
+    """`python -m nerf_attention.fit --quick` (fit.py:183-196) in a fresh process."""
+    kv = _quick_cache(tmp_path)
+    env = dict(os.environ, PYTHONPATH=str(ROOT / "nerf-attention_amd"))
+    r = subprocess.run([sys.executable, "-m", "nerf_attention.fit", "--kv_dir", str(kv),
+                        "--output_dir", str(tmp_path / "fits"), "--epochs", "20", "--quick",
+                        "--seed", "0"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = json.loads((tmp_path / "fits" / "fit_results.json").read_text())
+    _check_quick_outputs(golden_dir, recs, tmp_path / "fits")
+    ref_out = (golden_dir / "schema_quick" / "stdout.txt").read_text()
+    lines = _shape(r.stdout)
+    assert lines[:-1] == _shape(ref_out) + [""] and "sweep wall clock" in lines[-1]
+
+
+def test_farm_two_workers_equal_one_process(gpu):
+    """run_fits over two devices = two farm worker processes (here both on
+    GPU 0): every fit bitwise equal to training it in this process."""
+    from nerf_attention.synthetic import kv_slice
+    keys, vals = kv_slice(5, 1, seq_len=256)
+    cfgs = [SIRENConfig(64, 1, 30.0, "tiny"), SIRENConfig(128, 1, 30.0, "small"),
+            SIRENConfig(256, 2, 30.0, "medium"), SIRENConfig(64, 1, 30.0, "tiny")]
+    specs = []
+    for i, c in enumerate(cfgs):
+        torch.manual_seed(i)
+        specs.append(engine.FitSpec(target=keys if i % 2 else vals, config=c,
+                                    init=SIREN(c, 128).flat_parameters()))
+    farmed = engine.run_fits(specs, 40, devices=[0, 0])
+    for s, f in zip(specs, farmed):
+        alone = engine.run_fits([s], 40, devices=[0])[0]
+        assert torch.equal(alone.params.cpu(), f.params.cpu())
+        assert alone.losses == f.losses
+
+
+def test_forward_positions_autograd_and_short_inputs(gpu):
+    """SIREN.forward keeps autograd w.r.t. the positions and answers shapes
+    the engine does not take (one position) like the plain module."""
+    cfg = SIRENConfig(256, 2, 30.0, "medium")
+    torch.manual_seed(1)
+    m = SIREN(cfg, 128).cuda().eval()
+    m.requires_grad_(False)
+    x = torch.linspace(0, 1, 64, device="cuda").unsqueeze(1).requires_grad_(True)
+    y = m(x)
+    assert y.grad_fn is not None
+    y.sum().backward()
+    assert x.grad is not None and torch.isfinite(x.grad).all()
+    with torch.no_grad():
+        one = torch.tensor([[0.25]], device="cuda")
+        torch.testing.assert_close(m(one), m.network(one))

@@ -169,16 +169,18 @@ def test_plan_groups_by_width():
     cfgs = [SIRENConfig(256, 2, 30.0, "m"), SIRENConfig(64, 1, 30.0, "t"),
             SIRENConfig(256, 3, 30.0, "d"), SIRENConfig(256, 2, 60.0, "h")]
     specs = [engine.FitSpec(torch.zeros(128, 128), c, torch.zeros(1)) for c in cfgs]
-    groups = engine.plan_groups(specs, [0])
+    groups = engine.plan_groups(specs, 0)
     assert sorted(sorted(m) for _, m in groups) == [[0, 2, 3], [1]]
     assert groups[0][1] == [0, 2, 3]          # heaviest first
 
 
-def test_cpu_device_raises():
+def test_non_hip_device_raises():
+    """The engine path has no CPU fallback: only an explicit 'cpu' takes the
+    host path (test_host_path.py); any other non-HIP device raises."""
     from nerf_attention import fit_siren
     from nerf_attention._native import NerfhipError
     with pytest.raises(NerfhipError, match="no CPU"):
-        fit_siren(torch.zeros(64, 64), SIRENConfig(64, 1, 30.0, "t"), epochs=1, device="cpu",
+        fit_siren(torch.zeros(64, 64), SIRENConfig(64, 1, 30.0, "t"), epochs=1, device="meta",
                   verbose=False)
 
 
@@ -201,7 +203,7 @@ def test_plan_groups_chunks_large_groups():
     the sweep's 160-fit W=256 group becomes 4 x 40; small groups stay whole."""
     from nerf_attention.workloads import sweep_280
     _, specs = sweep_280(64, seed=0)
-    groups = engine.plan_groups(specs, [0])
+    groups = engine.plan_groups(specs, 0)
     sizes = sorted(len(m) for _, m in groups)
     assert sizes == [40] * 7
     assert sorted(i for _, m in groups for i in m) == list(range(280))

@@ -1,0 +1,134 @@
+"""BASELINE config 1 (`quickstart --cpu`) and the host-side pieces around the
+engine, on the CPU:
+
+* the explicit host path `fit_siren(..., device='cpu')` against the
+  reference's own 2000-epoch fits (tests/golden/fits_q512.json) and its
+  step-level parameters (steps_tiny.npz);
+* the quickstart pipeline through this package's public names (the ones
+  /root/reference/quickstart.py:8-15 imports) end to end on the CPU;
+* the CPU analysis path against the reference's per-slice analysis;
+* memory-bounded waves and the no-fallback rule for HIP requests.
+"""
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from nerf_attention import SIRENConfig, engine, fit_siren
+from nerf_attention.synthetic import kv_slice
+
+COS_TOL = 1e-3
+
+
+def test_host_fit_matches_reference_q512(golden_dir):
+    meta = json.loads((golden_dir / "fits_q512.json").read_text())
+    keys, vals = kv_slice(0, 0, seq_len=512, num_layers=4, num_kv_heads=4)
+    for name, t, cfg in (("key_tiny", keys, SIRENConfig(64, 1, 30.0, "tiny")),
+                         ("value_tiny", vals, SIRENConfig(64, 1, 30.0, "tiny"))):
+        torch.manual_seed(0)
+        r = fit_siren(t, cfg, epochs=2000, device="cpu", log_every=400, verbose=False)
+        ref = meta[name]
+        assert abs(r.final_cosine_mean - ref["final_cosine_mean"]) <= COS_TOL
+        assert r.num_parameters == ref["num_parameters"]
+        assert r.compression_ratio == pytest.approx(ref["compression_ratio"])
+        assert r.model.network[0].linear.weight.device.type == "cpu"
+
+
+def test_host_steps_match_reference(golden_dir):
+    z = np.load(golden_dir / "steps_tiny.npz")
+    cfg = SIRENConfig(64, 1, 30.0, "tiny")
+    t = torch.from_numpy(z["target"])
+    for k in (1, 3, 10):
+        torch.manual_seed(0)
+        r = fit_siren(t, cfg, epochs=k, device="cpu", verbose=False)
+        p = torch.cat([v.reshape(-1) for v in r.model.state_dict().values()]).numpy()
+        np.testing.assert_allclose(p, z[f"params_{k}"], atol=2.5e-4 * k)
+        assert np.mean(np.abs(p - z[f"params_{k}"]) <= 1e-6) >= 0.999
+        np.testing.assert_allclose(r.losses, z[f"losses_{k}"], rtol=1e-5)
+
+
+def test_host_verbose_lines(capsys):
+    keys, _ = kv_slice(0, 0, seq_len=128, num_layers=4, num_kv_heads=4)
+    fit_siren(keys, SIRENConfig(64, 1, 30.0, "tiny"), epochs=20, device="cpu", log_every=10)
+    lines = capsys.readouterr().out.strip().splitlines()
+    assert [l.split("|")[0].strip() for l in lines] == ["Epoch 10/20", "Epoch 20/20"]
+    assert all(len(l.split("|")) == 4 for l in lines)
+
+
+def test_quickstart_pipeline_cpu(tmp_path, golden_dir, capsys):
+    """quickstart.py:18-68's four steps through this package's names, on the
+    CPU (epochs cut to 30 to keep the CPU suite short)."""
+    from nerf_attention import (analyze_kv_cache, extract_kv_cache_synthetic, fit_kv_cache,
+                                generate_summary_figure, load_results, plot_pareto_frontier)
+    kv, an, fits, figs = (tmp_path / d for d in ("kv", "analysis", "fits", "figures"))
+    extract_kv_cache_synthetic(seq_len=512, num_layers=4, num_kv_heads=4, head_dim=128,
+                               output_dir=kv)
+    res = analyze_kv_cache(kv_dir=kv, output_dir=an, device="cpu")
+    assert (an / "analysis_results.json").exists() and len(res.layer_summaries) == 4
+    torch.manual_seed(0)
+    recs = fit_kv_cache(kv_dir=kv, output_dir=fits, epochs=30, device="cpu", quick=True)
+    ref = json.loads((golden_dir / "schema_quick" / "fit_results.json").read_text())
+    assert [r["name"] for r in recs] == [r["name"] for r in ref]
+    assert [list(r) for r in recs] == [list(r) for r in ref]
+    assert len(list(fits.glob("*_model.pt"))) == 6
+    figs.mkdir()
+    results = load_results(fits)
+    assert results == json.loads(json.dumps(recs))
+    plot_pareto_frontier(results, figs)
+    generate_summary_figure(results, figs)
+    assert list(figs.iterdir()) == []
+    out = capsys.readouterr().out
+    assert "[12/12] L3_H0_value_medium" in out and "RESULTS SUMMARY" in out
+
+
+def test_host_analysis_matches_reference(golden_dir):
+    """analyze_slices on CPU tensors (numpy + torch.linalg.svd) against the
+    reference's own per-slice analysis of the quickstart cache."""
+    from nerf_attention.analyze import analyze_slices, select_layers
+    from nerf_attention.synthetic import kv_layer
+    g = json.loads((golden_dir / "analysis_q512.json").read_text())
+    sh = g["shape"]
+    L, H = sh["num_layers"], sh["num_kv_heads"]
+    sl, names = [], []
+    for layer in select_layers(L):
+        t = kv_layer(layer, sh["seq_len"], L, H, sh["head_dim"], heads=range(min(H, 4)))
+        for h in range(min(H, 4)):
+            sl += [t["keys"][h], t["values"][h]]
+            names += [f"L{layer}_H{h}_K", f"L{layer}_H{h}_V"]
+    out = analyze_slices(torch.stack(sl), names)
+    for a in out:
+        b = g["slices"][a["name"]]
+        np.testing.assert_allclose(a["mean_autocorrelation"], b["mean_autocorrelation"],
+                                   atol=1e-6)
+        for k in b["spectral_energy"]:
+            assert abs(a["spectral_energy"][k] - b["spectral_energy"][k]) <= 1e-6
+        assert a["rank"]["effective_rank_99"] == b["rank"]["effective_rank_99"]
+        assert a["rank"]["full_rank"] == b["rank"]["full_rank"]
+
+
+def test_effective_rank_counts_min_n_d():
+    """A slice shorter than d_head has min(N, D) singular values (the
+    reference's torch.linalg.svd); the host path keeps that count."""
+    from nerf_attention.analyze import analyze_slices
+    x = torch.randn(1, 40, 64)
+    r = analyze_slices(x, ["short"])[0]["rank"]
+    assert r["full_rank"] == 40
+
+
+def test_hip_request_without_gpu_raises():
+    from nerf_attention._native import NerfhipError
+    if torch.cuda.is_available():
+        pytest.skip("host has a HIP device")
+    with pytest.raises(NerfhipError, match="HIP device"):
+        fit_siren(torch.zeros(64, 64), SIRENConfig(64, 1, 30.0, "t"), epochs=1, device="cuda",
+                  verbose=False)
+    with pytest.raises(NerfhipError):
+        engine.resolve_device("meta")
+
+
+def test_plan_waves():
+    assert engine.plan_waves([3, 3, 3], 100) == [[0, 1, 2]]
+    assert engine.plan_waves([60, 50, 30, 200, 10], 100) == [[0], [1, 2], [3], [4]]
+    assert engine.plan_waves([], 10) == []
