@@ -53,6 +53,7 @@ import torch.distributed as dist
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4
 BF16_MFMA_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 (no sparsity)
 PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16x3": BF16_MFMA_PEAK_TFLOPS / 6}
+HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E 8 TB/s
 RTX4060_FITS_PER_S = 0.232         # BASELINE.md §1 (280 fits / Σ train_time_seconds)
 GOLDEN_SWEEP = ROOT / "tests" / "golden" / "sweep_ref_seed0_e2000.json"
 PMC_TRAFFIC = ROOT / "profiles" / "pmc_traffic.json"
@@ -324,9 +325,24 @@ def main() -> None:
                              for i in mine)
             peak = PEAK[args.precision]
             job_tf = step_flops / (t_max / args.steps) / 1e12
+            hbm = None
+            if traffic:
+                # PMC bytes per launch (separate, serialised rocprofv3 passes of the
+                # same workload, tools/profile_round.sh) over this run's launch time
+                hbm = traffic["bytes"] / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "mfma", "achieved": round(achieved, 3),
                     "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "frac": round(achieved / peak, 4),
+                    "frac_kind": "dominant kernel, algorithmic FLOPs per launch / mean launch "
+                                 "duration in the timed region, where the width groups' "
+                                 "streams share the GPU (see isolated and job_frac)",
+                    "traffic": traffic and traffic["bytes"],
+                    "traffic_detail": traffic,
+                    "mfma_busy": traffic and traffic.get("mfma_busy"),
+                    "mfma_busy_kind": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GPU-active "
+                                      "cycles), rocprofv3 PMC pass (dispatches serialised)",
+                    "hbm_gbs": hbm and round(hbm, 1),
+                    "hbm_frac": hbm and round(hbm / HBM_PEAK_GBS, 4),
                     "kernel": f"{kname} [{args.precision}]",
                     "fits_per_launch": round(sum(x.n for x in job.groups
                                                  if f"<{x.W}," in kname) /
@@ -350,6 +366,10 @@ def main() -> None:
                     [specs[mine[i]] for i in g.members], kname, g_flops, args.precision, peak,
                     local)
                 roof["isolated"]["fits"] = g.n
+                if traffic:
+                    hi = traffic["bytes"] / (roof["isolated"]["avg_launch_ms"] * 1e-3) / 1e9
+                    roof["isolated"]["hbm_gbs"] = round(hi, 1)
+                    roof["isolated"]["hbm_frac"] = round(hi / HBM_PEAK_GBS, 4)
         parity = None
         if GOLDEN_SWEEP.exists() and args.epochs == 2000 and args.seq_len == 2048:
             ref = json.loads(GOLDEN_SWEEP.read_text())["records"]

@@ -548,11 +548,20 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
   constexpr int NDMA = SL / NTH;                                // DMAs every wave issues
   constexpr int QSTEP = (KT - 1) / 4 > 0 ? (KT - 1) / 4 : 1;
   typedef __attribute__((address_space(3))) void lds_void;
-  const int wave = tid >> 6;
-  // this lane's source offset (bf16) inside a sub-chunk, per DMA round
-  int soff[NPT];
+  // the wave index as an SGPR: every DMA's LDS destination (M0) is then SALU
+  // arithmetic instead of a per-instruction v_readfirstlane of a VGPR address
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // This lane's source offset (bf16) inside a sub-chunk for DMA round m.  With
+  // NTH = 256 the rounds step s = NTH/SR source rows; the swizzled offset of
+  // round m is that of round m % P plus (m / P)·P·s·KC, P = max(1, 16/s)
+  // (s = 8: rows r0 and r0 + 8 alternate, each pair of rounds is one plane),
+  // so only P per-lane offsets stay live and the rest is a compile-time
+  // addend on the SGPR sub-chunk offset.
+  constexpr int S_ROWS = NTH / SR, P = S_ROWS >= 16 ? 1 : 16 / S_ROWS;
+  static_assert(NTH % SR == 0 && 16 % (S_ROWS < 16 ? S_ROWS : 16) == 0, "DMA round layout");
+  int soff[P];
 #pragma unroll
-  for (int m = 0; m < NPT; ++m) {
+  for (int m = 0; m < P; ++m) {
     const int i = tid + NTH * m;
     const int row = (i / SR) & 15, pl = i / (16 * SR), ps = i % SR;
     soff[m] = (pl * 16 + row) * KC + 8 * (ps ^ (row & SWM));
@@ -566,8 +575,8 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
     uint16_t* buf = ring + (u % 3) * CH;
     if (SL % NTH == 0 || NTH * m + 64 * wave < SL)   // wave-uniform
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsrc, (lds_void*)(buf + 8 * (NTH * m + 64 * wave)), 16, 2 * soff[m], u * 96 * KC, 0,
-          0);
+          rsrc, (lds_void*)(buf + 8 * (NTH * m + 64 * wave)), 16, 2 * soff[m % P],
+          u * 96 * KC + 2 * (m / P) * P * S_ROWS * KC, 0, 0);
   };
   auto dma = [&](int u) {
 #pragma unroll

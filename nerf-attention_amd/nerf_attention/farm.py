@@ -37,11 +37,43 @@ def world() -> tuple:
     return 1, 0
 
 
-def rank_share(costs: list, n_ranks: int, rank: int) -> list:
-    """Indices of the fits rank `rank` trains (deterministic on every rank)."""
+def blocked_partition(costs: list, widths: list, n_bins: int) -> list:
+    """Bin per item: the items sorted by (width desc, cost desc, index) and cut
+    into n_bins contiguous runs of about equal total cost, so every bin holds
+    few widths and large same-width groups (one kernel launch per group per
+    epoch) instead of a sliver of every width."""
+    order = sorted(range(len(costs)), key=lambda i: (-widths[i], -costs[i], i))
+    total = float(sum(costs))
+    out = [0] * len(costs)
+    acc, b = 0.0, 0
+    for i in order:
+        # move to the next bin once this one holds its share (an item goes to
+        # the bin whose share boundary its midpoint falls before)
+        while b < n_bins - 1 and acc + 0.5 * costs[i] > total * (b + 1) / n_bins:
+            b += 1
+        out[i] = b
+        acc += costs[i]
+    return out
+
+
+PARTITIONS = ("lpt", "blocked")
+
+
+def rank_share(costs: list, n_ranks: int, rank: int, widths: list | None = None,
+               partition: str | None = None) -> list:
+    """Indices of the fits rank `rank` trains (deterministic on every rank).
+    partition: 'lpt' (longest processing time first over all fits) or
+    'blocked' (width-contiguous runs, needs `widths`); default
+    NERFHIP_FARM_PARTITION or 'lpt'."""
     if n_ranks <= 1:
         return list(range(len(costs)))
-    owner = lpt_partition(costs, n_ranks)
+    partition = partition or os.environ.get("NERFHIP_FARM_PARTITION", "lpt")
+    if partition == "blocked" and widths is not None:
+        owner = blocked_partition(costs, widths, n_ranks)
+    elif partition in PARTITIONS:
+        owner = lpt_partition(costs, n_ranks)
+    else:
+        raise ValueError(f"partition must be one of {PARTITIONS}, got {partition!r}")
     return [i for i, o in enumerate(owner) if o == rank]
 
 

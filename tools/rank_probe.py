@@ -26,15 +26,17 @@ def main():
     ap.add_argument("--epochs", type=int, default=200)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--all-ranks", action="store_true")
+    ap.add_argument("--partition", default="lpt")
     args = ap.parse_args()
     plan, specs = sweep_280(2048, seed=0)
     costs = [engine.fit_flops(2048, 128, s.config, args.epochs) for s in specs]
+    widths = [s.config.hidden_features for s in specs]
     engine.FitJob(specs[:8], 5, devices=[0]).launch()        # warm-up (module load)
     torch.cuda.synchronize()
     for n in [int(x) for x in args.worlds.split(",")]:
         times = []
         for r in (range(n) if args.all_ranks else [0]):
-            mine = farm.rank_share(costs, n, r)
+            mine = farm.rank_share(costs, n, r, widths, args.partition)
             job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[0])
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -43,7 +45,7 @@ def main():
             times.append(time.perf_counter() - t0)
             del job
         t = max(times)
-        print(json.dumps({"world": n, "epochs": args.epochs, "rank_s": [round(x, 3) for x in times],
+        print(json.dumps({"world": n, "partition": args.partition, "epochs": args.epochs, "rank_s": [round(x, 3) for x in times],
                           "pred_fits_per_s": round(280 / (t * 2000 / args.epochs), 2)}), flush=True)
 
 
