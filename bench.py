@@ -202,7 +202,8 @@ def dry_run(args, world: int, rank: int) -> None:
     with the rank count and the union of the shares (tests drive this on CPU)."""
     from nerf_attention import CONFIGS_FULL, engine, farm
     costs = [engine.fit_flops(args.seq_len, 128, c, args.epochs) for c in CONFIGS_FULL] * 40
-    mine = farm.rank_share(costs, world, rank)
+    widths = [c.hidden_features for c in CONFIGS_FULL] * 40
+    mine = farm.rank_share(costs, world, rank, widths)
     farm.barrier()
     t0 = time.perf_counter()
     share_flops = sum(costs[i] for i in mine)
@@ -264,7 +265,8 @@ def main() -> None:
     plan, specs = sweep_280(args.seq_len, seed=0)
     n_total = len(specs)
     costs = [engine.fit_flops(args.seq_len, 128, s.config, args.epochs) for s in specs]
-    mine = farm.rank_share(costs, world, rank)
+    widths = [s.config.hidden_features for s in specs]
+    mine = farm.rank_share(costs, world, rank, widths)
     job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[local],
                         precision=args.precision)
 
@@ -391,7 +393,9 @@ def main() -> None:
                                    "K/V on the reference's synthetic KV (32x8xNx128), "
                                    "seed-0 inits in reference order",
                        "seq_len": args.seq_len, "epochs": args.epochs, "fits": n_total,
-                       "parallelism": f"fit-farm over {world} GPU(s), LPT by FLOPs"},
+                       "parallelism": f"fit-farm over {world} GPU(s), "
+                                      f"{farm.auto_partition(world) if world > 1 else 'one'} "
+                                      f"partition by FLOPs, gloo control only"},
             "roofline": roof,
             "cos_delta_vs_ref": parity,
         }

@@ -1488,29 +1488,48 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
 // ---------------------------------------------------------------------------
 
 // target_mean = y.mean(0); target_std = y.std(0).clamp(min=1e-3);
-// targets_norm = (y − mean)/std   (siren.py:85-87).  One thread per column.
-__global__ void k_normalize(KArgs a) {
+// targets_norm = (y − mean)/std   (siren.py:85-87).  One workgroup per (64
+// columns, fit): lane = column (64 consecutive floats of a row: coalesced), the
+// 16 waves take every 16th row, fp64 partial sums are combined in a fixed
+// order through LDS (deterministic), then every thread normalises its rows.
+constexpr int kNormCols = 64, kNormRowGroups = 16;
+__global__ void __launch_bounds__(kNormCols * kNormRowGroups) k_normalize(KArgs a) {
+  __shared__ double part[kNormRowGroups][kNormCols];
   const int fit = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= a.D) return;
+  const int c = threadIdx.x & (kNormCols - 1), rg = threadIdx.x / kNormCols;
+  const int j = blockIdx.x * kNormCols + c;
+  const bool col = j < a.D;
   const float* T = a.target + fit * a.t_stride;
   float* TN = a.tnorm + fit * a.t_stride;
+  auto reduce = [&](double v) {     // Σ over the row groups, in order
+    part[rg][c] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int k = 0; k < kNormRowGroups; ++k) t += part[k][c];
+    __syncthreads();
+    return t;
+  };
   double s = 0.0;
-  for (int r = 0; r < a.N; ++r) s += (double)T[(int64_t)r * a.D + j];
-  const float mean = (float)(s / a.N);
+  if (col)
+    for (int r = rg; r < a.N; r += kNormRowGroups) s += (double)T[(int64_t)r * a.D + j];
+  const float mean = (float)(reduce(s) / a.N);
   double ss = 0.0;
-  for (int r = 0; r < a.N; ++r) {
-    const double d = (double)T[(int64_t)r * a.D + j] - (double)mean;
-    ss += d * d;
-  }
-  float sd = (float)sqrt(ss / (double)(a.N - 1));
+  if (col)
+    for (int r = rg; r < a.N; r += kNormRowGroups) {
+      const double d = (double)T[(int64_t)r * a.D + j] - (double)mean;
+      ss += d * d;
+    }
+  float sd = (float)sqrt(reduce(ss) / (double)(a.N - 1));
   sd = sd < 1e-3f ? 1e-3f : sd;
-  a.mean[fit * a.D + j] = mean;
-  a.stdv[fit * a.D + j] = sd;
-  for (int r = 0; r < a.n_pad; ++r) {
-    const int64_t o = (int64_t)r * a.D + j;
-    TN[o] = r < a.N ? (T[o] - mean) / sd : 0.f;
+  if (col && rg == 0) {
+    a.mean[fit * a.D + j] = mean;
+    a.stdv[fit * a.D + j] = sd;
   }
+  if (col)
+    for (int r = rg; r < a.n_pad; r += kNormRowGroups) {
+      const int64_t o = (int64_t)r * a.D + j;
+      TN[o] = r < a.N ? (T[o] - mean) / sd : 0.f;
+    }
 }
 
 // params_t ← transposed copies of every hidden weight and of the final weight
@@ -1816,7 +1835,8 @@ int prologue(GroupRun& r) {
   const size_t pbytes = (size_t)g->n_fits * r.s.params * sizeof(float);
   if (hipMemsetAsync(g->adam_m, 0, pbytes, r.st) != hipSuccess) return NERFHIP_ERR_LAUNCH;
   if (hipMemsetAsync(g->adam_v, 0, pbytes, r.st) != hipSuccess) return NERFHIP_ERR_LAUNCH;
-  hipLaunchKernelGGL(k_normalize, dim3((g->D + 127) / 128, g->n_fits), dim3(128), 0, r.st, r.a);
+  hipLaunchKernelGGL(k_normalize, dim3((g->D + kNormCols - 1) / kNormCols, g->n_fits),
+                     dim3(kNormCols * kNormRowGroups), 0, r.st, r.a);
   hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st, r.a);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }

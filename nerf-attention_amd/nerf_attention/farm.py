@@ -56,18 +56,30 @@ def blocked_partition(costs: list, widths: list, n_bins: int) -> list:
     return out
 
 
-PARTITIONS = ("lpt", "blocked")
+PARTITIONS = ("auto", "lpt", "blocked")
+
+
+def auto_partition(n_ranks: int) -> str:
+    """Measured on the 280-fit sweep (tools/rank_probe.py, every rank's share
+    alone on one MI355X, profiles/r02/rank_probe_*.log): width-blocked shares
+    win at 2 ranks (52.5 vs 49.5 predicted fits/s: each rank keeps 40-fit
+    groups), LPT wins from 4 ranks on (94 vs 88 at 4, 177 vs 148 at 8: a rank of
+    W=512 fits alone leaves the chip underused, a mix overlaps them with W=256
+    kernels on the other streams)."""
+    return "blocked" if n_ranks == 2 else "lpt"
 
 
 def rank_share(costs: list, n_ranks: int, rank: int, widths: list | None = None,
                partition: str | None = None) -> list:
     """Indices of the fits rank `rank` trains (deterministic on every rank).
-    partition: 'lpt' (longest processing time first over all fits) or
-    'blocked' (width-contiguous runs, needs `widths`); default
-    NERFHIP_FARM_PARTITION or 'lpt'."""
+    partition: 'lpt' (longest processing time first over all fits),
+    'blocked' (width-contiguous runs, needs `widths`) or 'auto'
+    (auto_partition); default NERFHIP_FARM_PARTITION or 'auto'."""
     if n_ranks <= 1:
         return list(range(len(costs)))
-    partition = partition or os.environ.get("NERFHIP_FARM_PARTITION", "lpt")
+    partition = partition or os.environ.get("NERFHIP_FARM_PARTITION", "auto")
+    if partition == "auto":
+        partition = auto_partition(n_ranks) if widths is not None else "lpt"
     if partition == "blocked" and widths is not None:
         owner = blocked_partition(costs, widths, n_ranks)
     elif partition in PARTITIONS:
@@ -202,8 +214,9 @@ def run_farm(specs: list, epochs: int, devices: list, lr: float = 1e-4, log_ever
         return []
     costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
              for s in specs]
+    widths = [s.config.hidden_features for s in specs]
     n = len(devices)
-    shares = [rank_share(costs, n, r) for r in range(n)]
+    shares = [rank_share(costs, n, r, widths) for r in range(n)]
     ctx = mp.get_context("spawn")
     jobs = []
     for r, dev in enumerate(devices):

@@ -50,15 +50,19 @@ def time_forward(model: SIREN, seq_len: int, device: str = 'cuda', warmup: int =
     around `runs` no-grad calls + synchronize (evaluate.py:187-200).  Device: the
     same calls bracketed by HIP events on the current stream."""
     positions = torch.linspace(0, 1, seq_len).unsqueeze(1).to(device)
+    on_gpu = positions.is_cuda
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     with torch.no_grad():
         for _ in range(warmup):
             model(positions)
-        torch.cuda.synchronize()
+        sync()
         start = time.perf_counter()
         for _ in range(runs):
             model(positions)
-        torch.cuda.synchronize()
+        sync()
         wall = (time.perf_counter() - start) / runs
+        if not on_gpu:        # a CPU model (the reference's device='cpu' case)
+            return wall * 1e3, wall * 1e3
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(runs):

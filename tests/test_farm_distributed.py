@@ -103,10 +103,27 @@ def test_bench_spawns_ranks_for_gpus_2():
     assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
     assert line["fits"] == list(range(280)) and set(line["owner"]) == {0, 1}
     costs = _costs()
-    assert [farm.rank_share(costs, 2, k) for k in (0, 1)] == \
+    widths = [c.hidden_features for c in CONFIGS_FULL] * 40
+    assert [farm.rank_share(costs, 2, k, widths) for k in (0, 1)] == \
         [[i for i, o in enumerate(line["owner"]) if o == k] for k in (0, 1)]
     lo, hi = sorted(line["rank_flops"])
     assert hi / lo < 1.05
+
+
+def test_partitions_cover_and_balance():
+    costs = _costs()
+    widths = [c.hidden_features for c in CONFIGS_FULL] * 40
+    for n in (2, 3, 4, 8):
+        for p in farm.PARTITIONS:
+            shares = [farm.rank_share(costs, n, r, widths, p) for r in range(n)]
+            assert sorted(i for s in shares for i in s) == list(range(280))
+            loads = [sum(costs[i] for i in s) for s in shares]
+            assert max(loads) / (sum(loads) / n) < 1.06, (n, p)
+    # blocked: each rank holds few widths
+    for r in range(2):
+        ws = {widths[i] for i in farm.rank_share(costs, 2, r, widths, "blocked")}
+        assert len(ws) <= 4
+    assert farm.auto_partition(2) == "blocked" and farm.auto_partition(8) == "lpt"
 
 
 def test_bench_rejects_world_mismatch():

@@ -71,7 +71,7 @@ def test_rank_share_vs_reference(gpu, golden_dir, sweep, world, rank):
     plan, specs = sweep
     ref = _ref_sweep(golden_dir)
     costs = [engine.fit_flops(2048, 128, s.config, 2000) for s in specs]
-    mine = farm.rank_share(costs, world, rank)
+    mine = farm.rank_share(costs, world, rank, [s.config.hidden_features for s in specs])
     outs = engine.run_fits([specs[i] for i in mine], 2000, devices=[0])
     d = np.array([abs(_cos(o) - ref[plan[i][0]]["final_cosine_mean"]) for i, o in zip(mine, outs)])
     assert d.max() <= COS_TOL, (d.max(), plan[mine[int(d.argmax())]][0])
@@ -203,3 +203,36 @@ def test_forward_positions_autograd_and_short_inputs(gpu):
     with torch.no_grad():
         one = torch.tensor([[0.25]], device="cuda")
         torch.testing.assert_close(m(one), m.network(one))
+
+
+REF_LATENCY_KEYS = ['name', 'config', 'siren_time_ms', 'hbm_time_4060_ms', 'hbm_time_h100_ms',
+                    'speedup_vs_4060', 'speedup_vs_h100', 'num_params']     # evaluate.py:206-215
+
+
+def test_latency_harness(gpu, tmp_path, capsys):
+    """evaluate.profile_latency / scaling._profile_siren_latency restated
+    (latency.py) on checkpoints written by the drop-in driver: record keys in
+    the reference's order (plus the MI355X fields), HBM times by the
+    reference's formula, one stdout line per model, latency_results.json."""
+    from nerf_attention import fit_kv_cache
+    from nerf_attention.latency import profile_latency, profile_siren_latency
+    kv = _quick_cache(tmp_path)
+    torch.manual_seed(0)
+    fit_kv_cache(kv, tmp_path / "fits", epochs=20, device="cuda", quick=True)
+    capsys.readouterr()
+    recs = profile_latency(tmp_path / "fits", tmp_path / "lat", device="cuda")
+    out = [l for l in capsys.readouterr().out.splitlines() if l.strip()]
+    assert len(recs) == 6 and len(out) == 6
+    saved = json.loads((tmp_path / "lat" / "latency_results.json").read_text())
+    assert saved == json.loads(json.dumps(recs))
+    raw = 512 * 128 * 2
+    for r, line in zip(recs, out):
+        assert list(r)[:8] == REF_LATENCY_KEYS
+        assert r["config"] == "medium" and r["num_params"] == 164992
+        assert r["hbm_time_4060_ms"] == pytest.approx(raw / 272e9 * 1000)
+        assert r["hbm_time_h100_ms"] == pytest.approx(raw / 3350e9 * 1000)
+        assert r["speedup_vs_4060"] == pytest.approx((raw / 272e9) / (r["siren_time_ms"] / 1e3))
+        assert 0 < r["siren_device_time_ms"] < 50 and 0 < r["siren_time_ms"] < 50
+        assert re.fullmatch(rf"  {r['name']}: SIREN=\d+\.\d{{3}}ms \| HBM\(4060\)=\d+\.\d{{3}}ms \| "
+                            rf"HBM\(H100\)=\d+\.\d{{3}}ms", line)
+    assert 0 < profile_siren_latency(tmp_path / "fits", 512, "cuda") < 50

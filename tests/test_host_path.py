@@ -132,3 +132,16 @@ def test_plan_waves():
     assert engine.plan_waves([3, 3, 3], 100) == [[0, 1, 2]]
     assert engine.plan_waves([60, 50, 30, 200, 10], 100) == [[0], [1, 2], [3], [4]]
     assert engine.plan_waves([], 10) == []
+
+
+def test_latency_harness_cpu(tmp_path):
+    """The latency harness on CPU checkpoints (the reference's device='cpu'
+    branch): no HIP synchronisation, same record keys."""
+    from nerf_attention.fit import _result_to_record, _save_model
+    from nerf_attention.latency import profile_latency
+    keys, _ = kv_slice(0, 0, seq_len=64, num_layers=4, num_kv_heads=4)
+    torch.manual_seed(0)
+    r = fit_siren(keys, SIRENConfig(64, 1, 30.0, "tiny"), epochs=3, device="cpu", verbose=False)
+    _save_model(tmp_path, "L0_H0_key_tiny", r, _result_to_record("L0_H0_key_tiny", 0, 0, "key", r))
+    recs = profile_latency(tmp_path, tmp_path / "lat", device="cpu")
+    assert len(recs) == 1 and recs[0]["num_params"] == 12608 and recs[0]["siren_time_ms"] > 0
