@@ -1,7 +1,11 @@
+# The exact default bench command under rocprofv3 --kernel-trace --stats (its
+# hipEvent kernel averages must agree with rocprof's), then the round profile
+# (200-epoch trace + FETCH/WRITE/MFMA PMC passes).  usage: tools/prof_default.sh <tag>
 set -u
-R="$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p "$R/gpurun_out/prof_default"
+R="$GRAFT_REPO_ROOT"; tag="${1:-r02}"; export TMPDIR=/tmp
+out="$R/gpurun_out/prof_default_$tag"; mkdir -p "$out"
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_default/trace" -o run --output-format csv -- python3 "$R/bench.py" > "$R/gpurun_out/prof_default/bench.log" 2>&1 || { echo "trace rc=$?"; tail "$R/gpurun_out/prof_default/bench.log"; exit 1; }
-find "$R/gpurun_out/prof_default/trace" -name '*kernel_stats.csv' -exec cp {} "$R/gpurun_out/prof_default/kernel_stats.csv" \;
-tail -1 "$R/gpurun_out/prof_default/bench.log" | cut -c1-400
-cd "$R" && bash tools/profile_round.sh x3q bf16x3
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 "$R/bench.py" > "$out/bench.log" 2>&1 || { echo "trace rc=$?"; tail "$out/bench.log"; exit 1; }
+find "$out/trace" -name '*kernel_stats.csv' -exec cp {} "$out/kernel_stats.csv" \;
+tail -1 "$out/bench.log" | cut -c1-600
+cd "$R" && bash tools/profile_round.sh "$tag" bf16x3
