@@ -13,7 +13,7 @@ import torch
 from .engine import FitSpec
 from .fit import select_fits, sweep_plan
 from .siren import SIREN
-from .synthetic import kv_layer
+from .synthetic import kv_cache
 from .types import KVMetadata
 
 LLAMA_SHAPE = dict(num_layers=32, num_kv_heads=8, head_dim=128)
@@ -29,10 +29,12 @@ def sweep_280(seq_len: int = 2048, seed: int | None = 0, quick: bool = False,
     meta = KVMetadata(model_name='synthetic', seq_len=seq_len, actual_tokens=seq_len,
                       **LLAMA_SHAPE)
     layers, heads, configs = select_fits(meta, quick, select, configs)
+    # every slice the selection reads, in one request (a process pool when large)
+    cache = kv_cache(layers, seq_len, LLAMA_SHAPE['num_layers'], LLAMA_SHAPE['num_kv_heads'],
+                     LLAMA_SHAPE['head_dim'], heads=range(heads))
 
     def load(layer):
-        return kv_layer(layer, seq_len, LLAMA_SHAPE['num_layers'], LLAMA_SHAPE['num_kv_heads'],
-                        LLAMA_SHAPE['head_dim'], heads=range(heads))
+        return cache[layer]
 
     plan, _ = sweep_plan(layers, heads, configs, load)
     if seed is not None:
