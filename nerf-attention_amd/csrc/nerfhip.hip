@@ -1683,9 +1683,20 @@ int launch_params(const KArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
+// NERFHIP_KIND splits a part further: 1 = row kernels only, 2 = parameter
+// kernels only (compiled with different flags, nerf_attention/_build.py), 0 = both
+#ifndef NERFHIP_KIND
+#define NERFHIP_KIND 0
+#endif
+#if NERFHIP_KIND == 1
+#define NERFHIP_INST_ONE(W, D, X) template int launch_rows<W, D, X>(const KArgs&, hipStream_t);
+#elif NERFHIP_KIND == 2
+#define NERFHIP_INST_ONE(W, D, X) template int launch_params<W, D, X>(const KArgs&, hipStream_t);
+#else
 #define NERFHIP_INST_ONE(W, D, X) \
   template int launch_rows<W, D, X>(const KArgs&, hipStream_t); \
   template int launch_params<W, D, X>(const KArgs&, hipStream_t);
+#endif
 #define NERFHIP_INST(W, X) NERFHIP_INST_ONE(W, 64, X) NERFHIP_INST_ONE(W, 128, X)
 #if NERFHIP_PART == 1
 NERFHIP_INST(64, false)

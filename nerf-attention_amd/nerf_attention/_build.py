@@ -34,10 +34,21 @@ def _stale() -> bool:
 
 N_PARTS = 9   # NERFHIP_PART 0 = host ABI + small kernels, 1..8 = (W, precision) kernels
 
+# Every (W, precision) part is compiled twice: its row kernels (NERFHIP_KIND=1)
+# and its parameter kernels (NERFHIP_KIND=2), so each gets its own flags.  The
+# parameter kernels' staging split (split3 + bf16 packing of 16 floats per
+# thread and block) is SLP-vectorised by default into v_pk_add_f32 plus the
+# register moves that pair its operands; packed fp32 VALU beside MFMAs costs
+# more than the scalar ops (MI355X_MICROARCH.md), and without it the W = 64..512
+# parameter kernels measured 3-10 % faster (profiles/r02/ab_noslp.log), while
+# the W = 256 row kernel measured ~2 % slower — so only the parameter side
+# drops SLP.
+KIND_FLAGS = {1: [], 2: ["-fno-slp-vectorize"]}
+
 
 def build(force: bool = False, verbose: bool = True) -> Path:
-    """Compile the nine NERFHIP_PART translation units in parallel (one per
-    hidden width × precision + the host part), then link them into
+    """Compile the NERFHIP_PART translation units in parallel (the host part,
+    then one per hidden width × precision × kernel kind), then link them into
     libnerfhip.so."""
     if not force and not _stale():
         return LIB
@@ -47,9 +58,12 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function", "-I", str(INCLUDE)]
     objs, procs = [], []
-    for part in range(N_PARTS):
-        obj = obj_dir / f"nerfhip_p{part}.o"
-        cmd = base + [f"-DNERFHIP_PART={part}", "-c", str(SOURCES[0]), "-o", str(obj)]
+    units = [(0, 0)] + [(part, kind) for part in range(1, N_PARTS) for kind in KIND_FLAGS]
+    for part, kind in units:
+        obj = obj_dir / (f"nerfhip_p{part}.o" if kind == 0 else f"nerfhip_p{part}k{kind}.o")
+        cmd = base + KIND_FLAGS.get(kind, []) + [f"-DNERFHIP_PART={part}",
+                                                 f"-DNERFHIP_KIND={kind}", "-c", str(SOURCES[0]),
+                                                 "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr, flush=True)
         procs.append(subprocess.Popen(cmd))

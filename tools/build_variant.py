@@ -29,13 +29,16 @@ def main():
     base = [_build.HIPCC, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC",
             "-Wno-unused-function", "-I", str(_build.INCLUDE), *rest]
     objs, procs = [], []
-    for part in range(_build.N_PARTS):
+    units = [(0, 0)] + [(p, k) for p in range(1, _build.N_PARTS) for k in _build.KIND_FLAGS]
+    for part, kind in units:
+        fname = f"nerfhip_p{part}.o" if kind == 0 else f"nerfhip_p{part}k{kind}.o"
         if part in parts:
-            obj = odir / f"nerfhip_p{part}.o"
-            procs.append(subprocess.Popen(base + [f"-DNERFHIP_PART={part}", "-c",
-                                                  str(_build.SOURCES[0]), "-o", str(obj)]))
+            obj = odir / fname
+            procs.append(subprocess.Popen(base + _build.KIND_FLAGS.get(kind, []) + [
+                f"-DNERFHIP_PART={part}", f"-DNERFHIP_KIND={kind}", "-c",
+                str(_build.SOURCES[0]), "-o", str(obj)]))
         else:
-            obj = _build.LIB_DIR / "obj" / f"nerfhip_p{part}.o"
+            obj = _build.LIB_DIR / "obj" / fname
         objs.append(obj)
     objs += [_build.LIB_DIR / "obj" / f"{s.stem}.o" for s in _build.SOURCES[1:]]
     if any(p.wait() != 0 for p in procs):
