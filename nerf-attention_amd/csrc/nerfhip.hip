@@ -535,7 +535,7 @@ __device__ __forceinline__ u4 ds_read16(uint32_t base) {
   return r;
 }
 
-template <int K, int JT, int NTH, int NST, int NLD, class Pre, class Elem, class Flush>
+template <int K, int JT, int NTH, int NST, int NLD, bool PIN, class Pre, class Elem, class Flush>
 __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, uint16_t* ring,
                                               const S8 (&b)[K / 32], int tid, int c, int g,
                                               Pre&& pre, Elem&& elem, Flush&& flush) {
@@ -651,6 +651,14 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
           if (kt == kq) elem(J - 1, q, acc_prev[q], pv_prev[q]);
         }
       }
+      // PIN (one wave per SIMD, W = 512): keep this k-step's MFMAs (and the
+      // epilogue VALU beside them) ahead of the wait for the next fragments.
+      // Left free, the scheduler sinks most MFMAs below the wait and the LDS
+      // read latency is exposed every k-step; at two waves per SIMD the other
+      // wave covers it and the free schedule measured 2 % faster (W = 256),
+      // at one wave per SIMD pinning measured 2.5 % faster (W = 512,
+      // profiles/r02/ab_pin_lgkm.log).
+      if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
       if constexpr (kt + 1 < KT) lgkm_wait(a_nxt);
       __builtin_amdgcn_sched_barrier(0);
       a_cur = a_nxt;
@@ -688,14 +696,14 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
 }
 
 // one GEMM phase in the kernel's precision (B: float[K/16][4] or S8[K/32])
-template <bool X3, int K, int JT, int NTH, int NST, int NLD, class B, class Pre, class Elem,
-          class Flush>
+template <bool X3, int K, int JT, int NTH, int NST, int NLD, bool PIN, class B, class Pre,
+          class Elem, class Flush>
 __device__ __forceinline__ void gemm_any(const void* src, float* lds, uint16_t* ring, const B& b,
                                          int tid, int c, int g, Pre&& pre, Elem&& elem,
                                          Flush&& flush) {
   if constexpr (X3)
-    gemm_phase_x3<K, JT, NTH, NST, NLD>(static_cast<const uint16_t*>(src), ring, b, tid, c, g, pre, elem,
-                         flush);
+    gemm_phase_x3<K, JT, NTH, NST, NLD, PIN>(static_cast<const uint16_t*>(src), ring, b, tid, c, g,
+                                             pre, elem, flush);
   else
     gemm_phase<K, JT, NTH>(static_cast<const float*>(src), lds, b, tid, c, g, pre, elem, flush);
 }
@@ -739,6 +747,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   constexpr int NWV = RowsCfg<W>::NWAVES, NTH = RowsCfg<W>::THREADS;
   constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
   constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
+  constexpr bool PIN = RowsCfg<W>::WAVES_PER_SIMD == 1;     // see gemm_phase_x3
   constexpr int WBUF_F = phase_lds_floats<W>() > phase_lds_floats<D>()
                              ? phase_lds_floats<W>() : phase_lds_floats<D>();
   constexpr int WBUF = X3 ? 0 : WBUF_F;   // fp32 weight ring, in floats (bf16x3: xring)
@@ -814,7 +823,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
     constexpr int K = (sizeof(bop) / sizeof(bop[0])) * (X3 ? 32 : 16);
 #pragma unroll
     for (int p = 0; p < NS; ++p) {
-      gemm_any<X3, K, JP, NTH, decltype(nst)::value, decltype(nld)::value>(
+      gemm_any<X3, K, JP, NTH, decltype(nst)::value, decltype(nld)::value, PIN>(
           static_cast<const char*>(src) + (int64_t)p * JP * K * (X3 ? 96 : 64), lds, xring, bop, tid,
           c, g, [&](int J) { return pre(p * JP + J); },
           [&](int J, int q, float acc, float pv) { out(p * JP + J, q, acc, pv); },
@@ -916,7 +925,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   S8 ys[JD / 2];
   float sq = 0.f;
   f4 y_pend;
-  gemm_any<X3, W, JD, NTH, TRAIN ? kTS : 0, TRAIN ? 1 : 0>(
+  gemm_any<X3, W, JD, NTH, TRAIN ? kTS : 0, TRAIN ? 1 : 0, PIN>(
       wsrc(false, L + 1), lds, xring, hb, tid, c, g,
       [&](int J) { return train ? ld4(T + 16 * J) : zero4; },
       [&](int J, int q, float acc, float t) {
