@@ -257,6 +257,11 @@ def main() -> None:
     farm.init_control_group()
     if args.dry_run:
         return dry_run(args, world, rank)
+    # one GPU per rank; more ranks than GPUs (a rehearsal of the N-rank path on
+    # a smaller box) share them round-robin.  device_count() does not
+    # initialise HIP.
+    n_dev = torch.cuda.device_count()
+    local = local % n_dev if n_dev else local
     torch.cuda.set_device(local)
 
     from nerf_attention import engine
@@ -387,6 +392,7 @@ def main() -> None:
             "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(value / RTX4060_FITS_PER_S, 2),
             "ranks_seen": world, "control_backend": "gloo" if world > 1 else None,
+            "devices_visible": torch.cuda.device_count(),
             "dtype": "f32" if args.precision == "fp32" else "f32 (bf16x3 split MFMA)",
             "precision": args.precision, "data": "synthetic",
             "config": {"workload": "280-fit sweep: 7 archs x layers{0,8,16,24,31} x heads0-3 x "
