@@ -193,9 +193,12 @@ __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out)
   float pc = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
   pc = fmaf(r2, pc, 4.166664568298827e-2f);
   pc = fmaf(r2 * r2, pc, fmaf(r2, -0.5f, 1.0f));
-  const bool swap = q & 1;
-  float s = swap ? pc : ps;
-  float c = swap ? ps : pc;
+  // (the same selects as bit operations — a bit-field insert for the swap, a
+  // sign xor from bits of q — compiled to fewer VALU but more live registers:
+  // 33 → 139 spilled VGPRs at W = 256, −7 % on the sweep, ab_perm_sincos_bits.log)
+  const bool swp = q & 1;
+  float s = swp ? pc : ps;
+  float c = swp ? ps : pc;
   s = (q & 2) ? -s : s;
   c = ((q + 1) & 2) ? -c : c;
   *s_out = s;
@@ -235,9 +238,12 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
   m = u1;
   l = __float_as_uint(r2);   // ≤ 8 significant bits: its top half is exact
 }
-// low half ← bf16 of a, high half ← bf16 of b (the top 16 bits of each)
+// low half ← bf16 of a, high half ← bf16 of b (the top 16 bits of each): one
+// v_perm_b32 (bytes 2,3 of a then bytes 2,3 of b; {S0,S1} = {b,a}) instead of
+// the shift / and / or the compiler otherwise emits.  Bitwise-equal results;
+// medium 40-fit row kernel −4 %, sweep unchanged (ab_perm_sincos_bits.log)
 __device__ __forceinline__ uint32_t pk_top(uint32_t a, uint32_t b) {
-  return (a >> 16) | (b & 0xffff0000u);
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
 __device__ __forceinline__ S8 split8(const float (&x)[8]) {
   uint32_t h[8], m[8], l[8];
