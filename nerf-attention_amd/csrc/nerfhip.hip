@@ -38,6 +38,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <math.h>
 #include <type_traits>
 
@@ -88,6 +89,8 @@ struct KArgs {
   int32_t x3;
   int64_t ws_stride;
   uint16_t* wsplit;
+  // row-step variant: 1 = the K-split kernel for small groups (k_step_rows_ks)
+  int32_t rows_ks;
 };
 template <int W, int D, bool X3> int launch_rows(const KArgs& a, hipStream_t st);
 template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t st);
@@ -1019,6 +1022,304 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
 }
 
 // ---------------------------------------------------------------------------
+// K-split row step for small groups (bf16x3, W >= 128, D = 128).
+//
+// k_step_rows gives one fit n_pad/64 workgroups, and each wave runs the whole
+// GEMM chain of its 16 rows: a lone fit (BASELINE config 2) keeps 32 CUs busy
+// and its epoch is that one serial chain.  Here the four waves of a workgroup
+// share ONE 16-row block and split every GEMM's reduction (k) dimension:
+// wave w owns the k-slices s ≡ w (mod 4) (32 features each) of every layer's
+// input, so it holds a quarter of the B operand and loads a quarter of each
+// weight tile straight from L2 into registers (PD items in flight, no LDS
+// staging, each weight element read once per workgroup).  Per output tile J:
+//   every wave: partial Zᵀ tile over its k-slices (6 bf16 MFMAs per slice)
+//               → LDS part[J&1][wave][q][lane]; one barrier per tile;
+//   finalize:   wave w sums the four partials of element q = w of every lane
+//               in wave order (deterministic) and runs the epilogue (bias,
+//               sincos, MSE/dL/dŷ, dZ = dH·cos·ω) on that element only — the
+//               epilogue VALU is split four ways too — then stores it to the
+//               scratch and to LDS out[J&1][q][lane];
+//   owner:      wave (J/2) mod 4, whose k-slice of the next phase contains
+//               tile J, reads the four elements back as its B-operand tile.
+// The scratch layout (H, dZ, G, dZ0 partials) is k_step_rows' own, so the
+// parameter kernel is shared; the cos map is private ([rblk][J][q][64 lanes]).
+// The k sums are grouped differently from k_step_rows (four partial chains),
+// so a fit's result depends on the row variant at the rounding level.
+// ---------------------------------------------------------------------------
+constexpr unsigned kKsDynLds = 81920;   // bytes of LDS padding per K-split workgroup
+template <int W> struct KsCfg {
+  static constexpr int PD = W >= 512 ? 8 : 6;   // A-fragment items (S8) in flight per wave
+};
+__host__ __device__ constexpr int ks_owner(int J) { return (J >> 1) & 3; }
+__host__ __device__ constexpr int ks_local(int J) { return 2 * (J >> 3) + (J & 1); }
+
+__device__ __forceinline__ void ks_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// A-fragment item i of a K-deep phase (tile J = i / NM, this wave's k-slice
+// s = w + 4·(i % NM)): three 16-B plane loads of the xoff layout, straight
+// from L2 into registers.
+template <int K> struct KsPhase {
+  static constexpr int KC = kc_of(K), NH = K / KC, KT = KC / 32, NM = K / 128;
+  static_assert(KT >= 4 && K % 128 == 0, "K-split needs K >= 128");
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff;
+  __device__ __forceinline__ KsPhase(const uint16_t* src, int c, int g, int w)
+      : rsrc(__builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000)),
+        voff(2 * (c * KC + 8 * g + 32 * w)) {}
+  template <int I> __device__ __forceinline__ S8 load() const {
+    constexpr int J = I / NM, m = I % NM;
+    constexpr int base = (J * NH + (4 * m) / KT) * 3 * 16 * KC + 32 * ((4 * m) % KT);
+    S8 r;
+    r.h = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * base, 0);
+    r.m = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 16 * KC), 0);
+    r.l = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 32 * KC), 0);
+    return r;
+  }
+};
+// the first PD items of a phase into the ring (issued a phase ahead)
+template <int K, int PD>
+__device__ __forceinline__ void ks_prefetch(S8 (&ring)[PD], const uint16_t* src, int c, int g,
+                                            int w) {
+  const KsPhase<K> ph(src, c, g, w);
+  static_for<0, PD>([&](auto ic_i) {
+    constexpr int i = decltype(ic_i)::value;
+    ring[i] = ph.template load<i>();
+  });
+}
+
+// One GEMM phase Zᵀ[JT·16][16 rows] = M[JT·16][K] · Hᵀ of the K-split kernel.
+// b: this wave's k-slices s = w + 4m of the input (K/128 of them).  ring
+// holds the phase's first PD items on entry (the previous phase issued them);
+// before its last epilogue the phase issues the first items of the next one
+// (next, KN deep; KN = 0: none).
+// pre(J) → a per-lane float loaded one tile ahead of fin; fin(J, acc, pv) →
+// the finalised element (feature 16J+4g+w, row c); own(J, f4) on the owner.
+template <int K, int JT, int PD, int KN, class Pre, class Fin, class Own>
+__device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ src, const S8 (&b)[K / 128],
+                                        S8 (&ring)[PD], const uint16_t* next, int w, int c, int g,
+                                        int lane, float* part, float* outb, Pre&& pre, Fin&& fin,
+                                        Own&& own) {
+  constexpr int NM = K / 128, NI = JT * NM;
+  static_assert(NI >= PD, "phase shorter than the prefetch depth");
+  const KsPhase<K> ph(src, c, g, w);
+  float pv_prev = 0.f;
+  const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  auto finalize = [&](int J, float pv) {
+    const float* p = part + (J & 1) * 1024 + w * 64 + lane;
+    const float acc = ((p[0] + p[256]) + p[512]) + p[768];
+    outb[(J & 1) * 256 + w * 64 + lane] = fin(J, acc, pv);
+  };
+  auto owner_read = [&](int J) {
+    if (w == ks_owner(J)) {
+      const float* o = outb + (J & 1) * 256 + lane;
+      const f4 v = {o[0], o[64], o[128], o[192]};
+      own(J, v);
+    }
+  };
+  static_for<0, JT>([&](auto Jc) {
+    constexpr int J = decltype(Jc)::value;
+    const float pv = pre(J);
+    f4 hi = zero4, lo = zero4;
+    static_for<0, NM>([&](auto mc) {
+      constexpr int m = decltype(mc)::value, i = J * NM + m;
+      mfma16x3(ring[i % PD], b[m], hi, lo);
+      if constexpr (i + PD < NI) ring[i % PD] = ph.template load<i + PD>();
+      if constexpr (J > 0 && m == 0) finalize(J - 1, pv_prev);
+    });
+    const f4 acc = hi + lo;
+    float* pw = part + (J & 1) * 1024 + w * 256 + lane;   // part[J&1][w][q][lane]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pw[q * 64] = acc[q];
+    pv_prev = pv;
+    ks_barrier();
+    if constexpr (J > 0) owner_read(J - 1);
+  });
+  if constexpr (KN > 0) {
+    if (next) ks_prefetch<KN>(ring, next, c, g, w);
+  }
+  finalize(JT - 1, pv_prev);
+  ks_barrier();
+  owner_read(JT - 1);
+}
+
+template <int W, int D>
+__global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
+  static_assert(W >= 128 && D == 128, "K-split rows: W >= 128, D = 128");
+  constexpr int JW = W / 16, JD = D / 16, PD = KsCfg<W>::PD;
+  constexpr int NO = W / 64;                 // owned tiles of a W-wide output
+  __shared__ __attribute__((aligned(16))) float part[2 * 4 * 4 * 64];
+  __shared__ __attribute__((aligned(16))) float outb[2 * 4 * 64];
+  __shared__ __attribute__((aligned(16))) float bias[2 * W];
+  __shared__ float lsum[4];
+  int fit, rblk;
+  if (!map_block(blockIdx.x, a.n_fits, a.n_pad / 16, fit, rblk)) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, g = lane >> 4;
+  const int L = a.fit_layers[fit];
+  const float om = a.fit_omega[fit];
+  const int r = rblk * 16 + c;
+  const bool valid = r < a.N;
+  // one instantiation for both modes: the forward-only mode (a.mode = 1) runs
+  // the same code with the stores and the backward skipped (see launch_rows)
+  const bool train = a.mode == 0;
+  const int n_pad = a.n_pad;
+  const float* P = a.params + fit * a.p_stride;
+  float* S = a.scratch + fit * a.s_stride;
+  const int64_t WN = (int64_t)W * n_pad;
+  float* SH = S;
+  float* SZ = S + (int64_t)(a.L_max + 1) * WN;
+  float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
+  float* SC = SG + (int64_t)D * n_pad;
+  const uint16_t* XS = a.wsplit + fit * a.ws_stride;
+  const int fe = 4 * g + w;                  // this wave's finalised feature inside a tile
+  // row-block-major scratch element (feature 16J+fe, row c)
+  const int64_t eoff = (int64_t)rblk * W * 16 + fe * 16 + c;
+  const int64_t coff = (int64_t)rblk * JW * 256 + w * 64 + lane;   // private cos map
+
+  float ho[NO][4];
+  S8 hs[W / 128];
+  S8 ys[1];
+  auto split_out = [&](auto nslices) {
+#pragma unroll
+    for (int m = 0; m < decltype(nslices)::value; ++m) hs[m] = split_pair(ho[2 * m], ho[2 * m + 1]);
+  };
+  auto own = [&](int J, f4 v) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ho[ks_local(J)][q] = v[q];
+  };
+  auto no_pre = [](int) { return 0.f; };
+  S8 ring[PD];                               // A-fragment items in flight
+  ks_prefetch<W>(ring, XS + xs_mat(W, D, L, false, 1), c, g, w);
+
+  // ---- layer 0 (K = 1, VALU): this wave's tiles J = 2s + h, s = w + 4m
+  stage_vec(bias, P, 2 * W, tid);
+  __syncthreads();
+  const float x = a.pos[r];
+  float* SHt = SH + (int64_t)rblk * W * 16 + g * 64 + (c & 3) * 16 + (c >> 2) * 4;
+#pragma unroll
+  for (int t = 0; t < NO; ++t) {
+    const int J = 2 * (w + 4 * (t >> 1)) + (t & 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 16 * J + 4 * g + q;
+      const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
+      float s, co;
+      sincos_fast(__fmul_rn(om, z), &s, &co);
+      ho[t][q] = s;
+    }
+    if (train) {
+      const f4 v = {ho[t][0], ho[t][1], ho[t][2], ho[t][3]};
+      sst4(SHt + J * 256, quad_transpose(v, c));
+    }
+  }
+  split_out(ic<W / 128>);
+  __syncthreads();
+
+  // ---- hidden SineLayers 1..L
+  for (int i = 1; i <= L; ++i) {
+    stage_vec(bias, P + off_hidden_w(W, i) + W * W, W, tid);
+    float* SHi = SH + (int64_t)i * WN + eoff;
+    float* SCi = SC + (int64_t)i * WN + coff;
+    gemm_ks<W, JW, PD, W>(
+        XS + xs_mat(W, D, L, false, i), hs, ring, XS + xs_mat(W, D, L, false, i + 1), w, c, g,
+        lane, part, outb, no_pre,
+        [&](int J, float acc, float) {
+          const float z = __fadd_rn(acc, bias[16 * J + fe]);
+          float s, co;
+          sincos_fast(__fmul_rn(om, z), &s, &co);
+          if (train) {
+            sst(SHi + J * 256, s);
+            sst(SCi + J * 256, co);
+          }
+          return s;
+        },
+        own);
+    split_out(ic<W / 128>);
+  }
+
+  // ---- final nn.Linear(W, D), MSE, dL/dŷ
+  stage_vec(bias, P + off_final_w(W, L) + W * D, D, tid);
+  const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + fe;
+  float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + fe : nullptr;
+  float* SGe = SG + (int64_t)rblk * D * 16 + fe * 16 + c;
+  float sq = 0.f;
+  gemm_ks<W, JD, PD, D>(
+      XS + xs_mat(W, D, L, false, L + 1), hs, ring, train ? XS + xs_mat(W, D, L, true, L + 1) : nullptr,
+      w, c, g,
+      lane, part, outb,
+      [&](int J) { return train ? T[16 * J] : 0.f; },
+      [&](int J, float acc, float t) {
+        const float y = __fadd_rn(acc, bias[16 * J + fe]);
+        if (yo) yo[16 * J] = y;
+        float gv = 0.f;
+        if (train) {
+          const float diff = y - t;
+          sq = valid ? fmaf(diff, diff, sq) : sq;
+          gv = valid ? a.grad_scale * diff : 0.f;
+          sst(SGe + J * 256, gv);
+        }
+        return gv;
+      },
+      own);
+  if (!train) return;
+  sq = wave_sum(sq);
+  if (lane == 0) lsum[w] = sq;
+  ys[0] = split_pair(ho[0], ho[1]);
+
+  // ---- backward: dZ = (dH ⊙ cos(ωz))·ω, stored for the weight gradients
+  // (the phase after W_iᵀ is W_{i-1}ᵀ, down to W_1ᵀ: xs_mat(.., true, i - 1))
+  auto bwd = [&](const uint16_t* Mt, const auto& bop, int layer, const uint16_t* next) {
+    const float* SCl = SC + (int64_t)layer * WN + coff;
+    float* SZl = SZ + (int64_t)layer * WN + eoff;
+    constexpr int K = (sizeof(bop) / sizeof(bop[0])) * 128;
+    gemm_ks<K, JW, PD, W>(
+        Mt, bop, ring, next, w, c, g, lane, part, outb, [SCl](int J) { return SCl[J * 256]; },
+        [&, SZl](int J, float acc, float cs) {
+          const float dz = __fmul_rn(__fmul_rn(acc, cs), om);
+          sst(SZl + J * 256, dz);
+          return dz;
+        },
+        own);
+    split_out(ic<W / 128>);
+  };
+  bwd(XS + xs_mat(W, D, L, true, L + 1), ys, L, XS + xs_mat(W, D, L, true, L));   // W_fᵀ [W][D]
+  for (int i = L; i >= 2; --i)
+    bwd(XS + xs_mat(W, D, L, true, i), hs, i - 1, XS + xs_mat(W, D, L, true, i - 1));
+  // layer 0: cos(ω(x·w0 + b0)) recomputed; dZ0 reduced over the 16 rows at once
+  stage_vec(bias, P, 2 * W, tid);
+  float* PZ = SZ + (int64_t)rblk * 2 * W;
+  gemm_ks<W, JW, PD, 0>(
+      XS + xs_mat(W, D, L, true, 1), hs, ring, nullptr, w, c, g, lane, part, outb, no_pre,
+      [&](int J, float acc, float) {
+        const int f = 16 * J + fe;
+        const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
+        float s, co;
+        sincos_fast(__fmul_rn(om, z), &s, &co);
+        const float dz = __fmul_rn(__fmul_rn(acc, co), om);
+        float sx = __fmul_rn(dz, x), s1 = dz;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+          sx += __shfl_xor(sx, o, 64);
+          s1 += __shfl_xor(s1, o, 64);
+        }
+        if (c == 0) {
+          sst(PZ + f, sx);
+          sst(PZ + W + f, s1);
+        }
+        return 0.f;
+      },
+      [](int, f4) {});
+  if (tid == 0)
+    a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] =
+        ((lsum[0] + lsum[1]) + lsum[2]) + lsum[3];
+}
+
+// ---------------------------------------------------------------------------
 // Parameter-parallel step: weight/bias gradients reduced over all rows, then
 // Adam.  Tiles per fit: L·(W/T)² hidden + (D/TD)(W/T) final + W/64 first.
 //
@@ -1628,6 +1929,7 @@ int validate(int W, int D, int N, int L_max, int epochs) {
   return NERFHIP_OK;
 }
 
+constexpr int64_t kMaxSplit = 8;
 void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   const int64_t n_pad = ((int64_t)N + kRowPad - 1) / kRowPad * kRowPad;
   s->n_pad = n_pad;
@@ -1638,14 +1940,47 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   s->stats = D;
   s->loss_partial = (int64_t)epochs * (n_pad / 16);
   s->rows = n_pad;
-  // split-K row slices for small groups: the largest power of two <= 8 that
-  // leaves every slice an even number (>= 4) of 16-row blocks
+  // split-K row slices for small groups: the largest power of two <= kMaxSplit
+  // that leaves every slice an even number (>= 4) of 16-row blocks (the
+  // workspace is sized for it; make_args may use fewer slices)
   const int64_t nb = n_pad / 16;
   int64_t sp = 1;
-  while (sp < 8 && nb % (4 * sp) == 0 && nb / (2 * sp) >= 4) sp *= 2;
+  while (sp < kMaxSplit && nb % (4 * sp) == 0 && nb / (2 * sp) >= 4) sp *= 2;
   s->grad_split = sp;
   s->grad_partial = sp * s->params;
   s->wsplit = xs_size(W, D, L_max);
+}
+
+// Row slices of a small group's split-K gradient reduction: the workspace's
+// grad_split, capped at NERFHIP_GRAD_SPLIT_MAX (default kDefSplit).  (16
+// slices with a 16-slice workspace measured: one medium fit's parameter
+// kernel −9 %, five large fits +40 %, one wide fit at 8192 +9 %: not kept.)
+constexpr int kDefSplit = 8;
+int32_t split_for(const nerfhip_group* g, const nerfhip_sizes& s) {
+  (void)g;
+  const char* e = getenv("NERFHIP_GRAD_SPLIT_MAX");
+  const int64_t cap = e ? atoi(e) : kDefSplit;
+  int64_t sp = s.grad_split;
+  while (sp > 1 && sp > cap) sp /= 2;
+  return (int32_t)sp;
+}
+
+// Row-step variant of a group.  The K-split kernel (k_step_rows_ks) gives a
+// fit 4x the waves and a quarter of the serial GEMM chain per wave, at 4x the
+// weight reads per row and one barrier per output tile: it pays only while the
+// regular kernel leaves most CUs idle, i.e. for groups whose regular grid
+// (n_fits · n_pad/64 workgroups) is below kKsMaxWorkgroups.  Measured (rows
+// kernel, bf16x3): one medium fit at 2048 (32 regular workgroups) 0.092 →
+// 0.067 ms; 8 medium fits 0.096 → 0.254; 5 large fits 0.29 → 0.62; one wide
+// fit at 8192 (128) 0.36 → 0.59.  NERFHIP_ROWS_KS = 0 / 1 forces the choice
+// (supported shapes only: bf16x3, W >= 128, D = 128).
+constexpr int64_t kKsMaxWorkgroups = 48;
+bool rows_ks_for(const nerfhip_group* g, const nerfhip_sizes& s) {
+  if (g->precision != NERFHIP_PRECISION_BF16X3 || g->W < 128 || g->D != 128) return false;
+  const char* e = getenv("NERFHIP_ROWS_KS");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return (int64_t)g->n_fits * (s.n_pad / kRowPad) < kKsMaxWorkgroups;
 }
 
 KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
@@ -1661,12 +1996,13 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   // F.mse_loss backward: grad = (2/numel)·(ŷ−y), the 2/numel a python float
   // rounded to fp32 (TORCH/_decomp/decompositions.py:393-397).
   a.grad_scale = (float)(2.0 / ((double)g->N * (double)g->D));
-  a.n_split = (g->grad_partial && g->n_fits < kXcdMinFits) ? (int32_t)s.grad_split : 1;
+  a.n_split = (g->grad_partial && g->n_fits < kXcdMinFits) ? split_for(g, s) : 1;
   a.gp_stride = s.grad_partial;
   a.gpart = g->grad_partial;
   a.x3 = g->precision == NERFHIP_PRECISION_BF16X3;
   a.ws_stride = s.wsplit;
   a.wsplit = static_cast<uint16_t*>(g->wsplit);
+  a.rows_ks = rows_ks_for(g, s) ? 1 : 0;
   return a;
 }
 
@@ -1676,6 +2012,23 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
 namespace nerfhip_detail {
 template <int W, int D, bool X3>
 int launch_rows(const KArgs& a, hipStream_t st) {
+  if constexpr (X3 && W >= 128 && D == 128) {
+    if (a.rows_ks) {
+      const int grid = grid_for(a.n_fits, a.n_pad / 16);
+      // One K-split workgroup per CU: dynamic LDS padding keeps a second one
+      // off the CU.  A separate forward-only instantiation (TRAIN = false)
+      // gave wrong rows in ~5 % of the workgroups that shared a CU with
+      // another one (seq 8192, reproducible; gone with 96 KB of padding, not
+      // with 4 KB); the single runtime-mode kernel measured correct with and
+      // without sharing (tools/ks_diag4.py).  The cause was not isolated, so
+      // the kernel keeps a CU to itself; below kKsMaxWorkgroups the grid is
+      // under the CU count and the padding costs nothing.
+      const char* e = getenv("NERFHIP_KS_DYN_LDS");
+      const unsigned dyn = e ? (unsigned)atoi(e) : kKsDynLds;
+      hipLaunchKernelGGL((k_step_rows_ks<W, D>), dim3(grid), dim3(256), dyn, st, a);
+      return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+    }
+  }
   const int grid = grid_for(a.n_fits, a.n_pad / RowsCfg<W>::ROWS);
   if (a.mode == 0)
     hipLaunchKernelGGL((k_step_rows<W, D, X3, true>), dim3(grid), dim3(RowsCfg<W>::THREADS), 0,
