@@ -1033,12 +1033,12 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
 // weight tile straight from L2 into registers (PD items in flight, no LDS
 // staging, each weight element read once per workgroup).  Per output tile J:
 //   every wave: partial Zᵀ tile over its k-slices (6 bf16 MFMAs per slice)
-//               → LDS part[J&1][wave][q][lane]; one barrier per tile;
+//               → LDS part[slot][wave][q][lane]; one barrier per tile pair;
 //   finalize:   wave w sums the four partials of element q = w of every lane
 //               in wave order (deterministic) and runs the epilogue (bias,
 //               sincos, MSE/dL/dŷ, dZ = dH·cos·ω) on that element only — the
 //               epilogue VALU is split four ways too — then stores it to the
-//               scratch and to LDS out[J&1][q][lane];
+//               scratch and to LDS out[slot][q][lane];
 //   owner:      wave (J/2) mod 4, whose k-slice of the next phase contains
 //               tile J, reads the four elements back as its B-operand tile.
 // The scratch layout (H, dZ, G, dZ0 partials) is k_step_rows' own, so the
@@ -1106,43 +1106,58 @@ __device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ src, const 
   constexpr int NM = K / 128, NI = JT * NM;
   static_assert(NI >= PD, "phase shorter than the prefetch depth");
   const KsPhase<K> ph(src, c, g, w);
-  float pv_prev = 0.f;
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+  // tiles go in pairs, one barrier per pair: LDS slot of tile J = 2·(pair parity) + (J & 1)
+  auto slot = [](int J) { return 2 * ((J >> 1) & 1) + (J & 1); };
   auto finalize = [&](int J, float pv) {
-    const float* p = part + (J & 1) * 1024 + w * 64 + lane;
+    const float* p = part + slot(J) * 1024 + w * 64 + lane;
     const float acc = ((p[0] + p[256]) + p[512]) + p[768];
-    outb[(J & 1) * 256 + w * 64 + lane] = fin(J, acc, pv);
+    outb[slot(J) * 256 + w * 64 + lane] = fin(J, acc, pv);
   };
   auto owner_read = [&](int J) {
     if (w == ks_owner(J)) {
-      const float* o = outb + (J & 1) * 256 + lane;
+      const float* o = outb + slot(J) * 256 + lane;
       const f4 v = {o[0], o[64], o[128], o[192]};
       own(J, v);
     }
   };
-  static_for<0, JT>([&](auto Jc) {
-    constexpr int J = decltype(Jc)::value;
-    const float pv = pre(J);
-    f4 hi = zero4, lo = zero4;
-    static_for<0, NM>([&](auto mc) {
-      constexpr int m = decltype(mc)::value, i = J * NM + m;
-      mfma16x3(ring[i % PD], b[m], hi, lo);
-      if constexpr (i + PD < NI) ring[i % PD] = ph.template load<i + PD>();
-      if constexpr (J > 0 && m == 0) finalize(J - 1, pv_prev);
+  static_assert(JT % 2 == 0, "tile pairs");
+  float pv_prev[2] = {0.f, 0.f};
+  static_for<0, JT / 2>([&](auto Pc) {
+    constexpr int Pp = decltype(Pc)::value;
+    const float pv[2] = {pre(2 * Pp), pre(2 * Pp + 1)};
+    f4 acc[2];
+    static_for<0, 2>([&](auto tc) {
+      constexpr int t = decltype(tc)::value, J = 2 * Pp + t;
+      f4 hi = zero4, lo = zero4;
+      static_for<0, NM>([&](auto mc) {
+        constexpr int m = decltype(mc)::value, i = J * NM + m;
+        mfma16x3(ring[i % PD], b[m], hi, lo);
+        if constexpr (i + PD < NI) ring[i % PD] = ph.template load<i + PD>();
+        if constexpr (Pp > 0 && m == 0) finalize(J - 2, pv_prev[t]);
+      });
+      acc[t] = hi + lo;
     });
-    const f4 acc = hi + lo;
-    float* pw = part + (J & 1) * 1024 + w * 256 + lane;   // part[J&1][w][q][lane]
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pw[q * 64] = acc[q];
-    pv_prev = pv;
+    for (int t = 0; t < 2; ++t) {
+      float* pw = part + slot(2 * Pp + t) * 1024 + w * 256 + lane;   // part[slot][w][q][lane]
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pw[q * 64] = acc[t][q];
+      pv_prev[t] = pv[t];
+    }
     ks_barrier();
-    if constexpr (J > 0) owner_read(J - 1);
+    if constexpr (Pp > 0) {
+      owner_read(2 * Pp - 2);
+      owner_read(2 * Pp - 1);
+    }
   });
   if constexpr (KN > 0) {
     if (next) ks_prefetch<KN>(ring, next, c, g, w);
   }
-  finalize(JT - 1, pv_prev);
+  finalize(JT - 2, pv_prev[0]);
+  finalize(JT - 1, pv_prev[1]);
   ks_barrier();
+  owner_read(JT - 2);
   owner_read(JT - 1);
 }
 
@@ -1151,8 +1166,8 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   static_assert(W >= 128 && D == 128, "K-split rows: W >= 128, D = 128");
   constexpr int JW = W / 16, JD = D / 16, PD = KsCfg<W>::PD;
   constexpr int NO = W / 64;                 // owned tiles of a W-wide output
-  __shared__ __attribute__((aligned(16))) float part[2 * 4 * 4 * 64];
-  __shared__ __attribute__((aligned(16))) float outb[2 * 4 * 64];
+  __shared__ __attribute__((aligned(16))) float part[4 * 4 * 4 * 64];   // [slot][wave][q][lane]
+  __shared__ __attribute__((aligned(16))) float outb[4 * 4 * 64];       // [slot][q][lane]
   __shared__ __attribute__((aligned(16))) float bias[2 * W];
   __shared__ float lsum[4];
   int fit, rblk;

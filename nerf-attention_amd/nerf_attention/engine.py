@@ -105,6 +105,19 @@ def resolve_device(device) -> torch.device:
 
 
 SPLIT_MAX_FITS = 8   # libnerfhip splits the gradient reduction of groups below this size
+# ... but only while the fused one-pass grid (one workgroup per weight tile and
+# fit) stays under SPLIT_MIN_TILES workgroups: 5 large fits (220 tiles) train
+# faster fused (parameter kernel 0.17 -> 0.14 ms, 8-rank share prediction
+# 168 -> 185 fits/s), 5 small fits (20 tiles) 3.5x slower fused
+# (profiles/r02/split_probe.log)
+SPLIT_MIN_TILES = 128
+
+
+def param_tiles(W: int, D: int, L: int) -> int:
+    """Workgroups of one fit's parameter step (nerfhip.hip ParamsCfg::tiles)."""
+    T = min(W, 128)
+    nt = W // T
+    return L * nt * nt + (D // min(D, T)) * nt + W // 64
 
 # GEMM arithmetic of the engine (include/nerfhip.h nerfhip_precision):
 #   "fp32"   exact fp32 MFMA (v_mfma_f32_*_f32), the reference's arithmetic;
@@ -187,8 +200,11 @@ class _Group:
         self.row_sq = torch.empty(n, n_pad, **f32)
         # groups of < SPLIT_MAX_FITS fits reduce the weight gradient in row
         # slices (nerfhip.h grad_partial); the sweep's groups never need it
+        split_max = int(os.environ.get("NERFHIP_SPLIT_MAX_FITS", SPLIT_MAX_FITS))
+        small = n * param_tiles(self.W, self.D, self.L_max) < SPLIT_MIN_TILES
         self.grad_partial = torch.empty(n, int(s.grad_partial), **f32) \
-            if split and n < SPLIT_MAX_FITS and s.grad_split > 1 else None
+            if (split and n < min(split_max, SPLIT_MAX_FITS) and s.grad_split > 1
+                and (small or "NERFHIP_SPLIT_MAX_FITS" in os.environ)) else None
         self.wsplit = torch.empty(n, int(s.wsplit), dtype=torch.int16, device=dev) \
             if precision == "bf16x3" else None
         if self.n_probe:

@@ -66,8 +66,9 @@ def test_sweep_280_vs_reference(gpu, golden_dir, sweep):
 def test_rank_share_vs_reference(gpu, golden_dir, sweep, world, rank):
     """What one rank of a `world`-GPU farm trains, alone on one GPU: its
     groups are smaller (at 8 ranks the W = 512, 128 and 64 groups hold 5 fits
-    each, so their weight gradients take the split-K path), yet every fit
-    stays within 1e-3."""
+    each; the W = 128 and 64 ones are small enough to take the split-K
+    weight-gradient path, engine.SPLIT_MIN_TILES), yet every fit stays within
+    1e-3."""
     plan, specs = sweep
     ref = _ref_sweep(golden_dir)
     costs = [engine.fit_flops(2048, 128, s.config, 2000) for s in specs]
@@ -78,7 +79,7 @@ def test_rank_share_vs_reference(gpu, golden_dir, sweep, world, rank):
     if world == 8:
         job = engine.FitJob([specs[i] for i in mine], 1, devices=[0])
         split = {g.W for g in job.groups if g.grad_partial is not None}
-        assert split == {512, 128, 64}                 # the split-K path ran
+        assert split == {128, 64}                      # the split-K path ran
 
 
 @pytest.mark.parametrize("seq_len", [512, 1024, 4096])

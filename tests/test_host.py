@@ -210,3 +210,16 @@ def test_plan_groups_chunks_large_groups():
     assert [len(c) for c in engine._chunks(list(range(100)), 40)] == [32, 32, 36]
     assert [len(c) for c in engine._chunks(list(range(9)), 40)] == [9]
     assert [len(c) for c in engine._chunks(list(range(160)), 0)] == [160]
+
+
+def test_param_tiles_matches_kernel_grid():
+    """engine.param_tiles restates nerfhip.hip ParamsCfg::tiles (the fused
+    parameter-step grid per fit), which decides split-K for small groups."""
+    from nerf_attention import engine
+    assert engine.param_tiles(256, 128, 2) == 14      # medium: 2·4 hidden + 2 final + 4 first-layer
+    assert engine.param_tiles(512, 128, 2) == 44      # large
+    assert engine.param_tiles(512, 128, 3) == 60      # wide (512, 3)
+    assert engine.param_tiles(128, 128, 1) == 4       # small
+    assert engine.param_tiles(64, 128, 1) == 4        # tiny
+    assert 5 * engine.param_tiles(512, 128, 2) >= engine.SPLIT_MIN_TILES    # 8-rank large group: fused
+    assert engine.param_tiles(256, 128, 2) < engine.SPLIT_MIN_TILES         # config 2: split-K
