@@ -1633,10 +1633,12 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           adam_update(p, mm, vv, gsum, step_size, bc2s);
           P[idx] = p; M[idx] = mm; V[idx] = vv;
           split3(p, th[qq], tm[qq], tl[qq]);
+#ifndef NERFHIP_EXP_NO_FWDCOPY   // diagnostic build only: timing of the copy's stores
           // forward copy M[j][kcol] of [out_dim][W]
           XS[xf + xoff(out_dim, W, j, kcol, 0)] = (uint16_t)(th[qq] >> 16);
           XS[xf + xoff(out_dim, W, j, kcol, 1)] = (uint16_t)(tm[qq] >> 16);
           XS[xf + xoff(out_dim, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
+#endif
         }
         if (!G) {   // transposed copy: Mᵀ[kcol][j..j+3] is one 8-B run per plane
           const int jb = jrow0 + 8 * qb + 4 * h;
