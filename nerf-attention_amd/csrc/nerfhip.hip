@@ -1946,7 +1946,7 @@ int validate(int W, int D, int N, int L_max, int epochs) {
   return NERFHIP_OK;
 }
 
-constexpr int64_t kMaxSplit = 8;
+constexpr int64_t kMaxSplit = 16;
 void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   const int64_t n_pad = ((int64_t)N + kRowPad - 1) / kRowPad * kRowPad;
   s->n_pad = n_pad;
@@ -1968,17 +1968,26 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   s->wsplit = xs_size(W, D, L_max);
 }
 
-// Row slices of a small group's split-K gradient reduction: the workspace's
-// grad_split, capped at NERFHIP_GRAD_SPLIT_MAX (default kDefSplit).  (16
-// slices with a 16-slice workspace measured: one medium fit's parameter
-// kernel −9 %, five large fits +40 %, one wide fit at 8192 +9 %: not kept.)
-constexpr int kDefSplit = 8;
+// Row slices of a small group's split-K gradient reduction: the most the
+// workspace allows (grad_split, <= 16) while the split grid, fits × weight
+// tiles × slices, stays within kSplitGrid workgroups (two per CU), or
+// NERFHIP_GRAD_SPLIT_MAX.  Measured (profiles/r02/ab_rows_ks.log "split 16"):
+// one medium fit (14 tiles) 8 → 16 slices −9 % parameter-kernel time; one
+// wide fit at 8192 (60 tiles) 16 slices +9 % (the grid passes 512 there).
+constexpr int64_t kSplitGrid = 512;
+int64_t param_tiles(int W, int D, int L) {   // ParamsCfg<W, D, X3>::tiles(L)
+  const int T = W < 128 ? W : 128, nt = W / T, TD = D < T ? D : T;
+  return (int64_t)L * nt * nt + (int64_t)(D / TD) * nt + W / 64;
+}
 int32_t split_for(const nerfhip_group* g, const nerfhip_sizes& s) {
-  (void)g;
   const char* e = getenv("NERFHIP_GRAD_SPLIT_MAX");
-  const int64_t cap = e ? atoi(e) : kDefSplit;
   int64_t sp = s.grad_split;
-  while (sp > 1 && sp > cap) sp /= 2;
+  if (e) {
+    while (sp > 1 && sp > atoi(e)) sp /= 2;
+  } else {
+    const int64_t grid = (int64_t)g->n_fits * param_tiles(g->W, g->D, g->L_max);
+    while (sp > 2 && grid * sp > kSplitGrid) sp /= 2;
+  }
   return (int32_t)sp;
 }
 

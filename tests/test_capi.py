@@ -62,10 +62,10 @@ def test_group_sizes(lib, W, D, N, L, E):
     assert s.scratch == 3 * (L + 1) * W * n_pad + D * n_pad
     assert s.target == n_pad * D and s.rows == n_pad
     assert s.loss_partial == E * n_pad // 16
-    nb, sp = n_pad // 16, 1           # split-K slices: even, >= 4 blocks each, <= 8
-    while sp < 8 and nb % (4 * sp) == 0 and nb // (2 * sp) >= 4:
+    nb, sp = n_pad // 16, 1           # split-K slices: even, >= 4 blocks each, <= 16
+    while sp < 16 and nb % (4 * sp) == 0 and nb // (2 * sp) >= 4:
         sp *= 2
-    assert s.grad_split == sp == {2048: 8, 192: 2}[n_pad]
+    assert s.grad_split == sp == {2048: 16, 192: 2}[n_pad]
     assert s.grad_partial == sp * s.params
     assert s.wsplit == 6 * (L * W * W + W * D)        # bf16x3 split planes, fwd + transposed
 
