@@ -1504,7 +1504,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // transposed fp32 copy, both split copies of the weights for the row kernel.
 constexpr int kFx = 24;
 
-template <int TJ, int TK, int NW>
+template <int TJ, int TK, int NW, int WW, int OD>
 __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
                                            const float* __restrict__ B, int FB, int j0, int k0,
                                            int rb0, int n_blocks, float* G, float* P, float* M,
@@ -1519,7 +1519,13 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   constexpr int PLX = (TJ + TK) * kFx, BUFX = 3 * PLX;
   static_assert(NA >= 1 && NB >= 1 && NPA >= 1, "tile too small for the wave grid");
   uint16_t* lds = reinterpret_cast<uint16_t*>(lds_f);
-  const int W = a.W;
+  // W and out_dim at compile time (the kernel's template W, and W or D):
+  // the xoff() split-copy addresses fold to shifts and masks instead of
+  // runtime integer divisions in the Adam epilogue (parameter kernel −0.8 %,
+  // 200-epoch sweep +0.5 %, profiles/r02/ab_params_ct_width.log)
+  constexpr int W = WW, kOD = OD;
+  (void)a;
+  (void)out_dim;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wj = wave / WK, wk = wave % WK, h = lane >> 5, lr = lane & 31;
   const int64_t sA = (int64_t)FA * 16, sB = (int64_t)FB * 16;
@@ -1635,9 +1641,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           split3(p, th[qq], tm[qq], tl[qq]);
 #ifndef NERFHIP_EXP_NO_FWDCOPY   // diagnostic build only: timing of the copy's stores
           // forward copy M[j][kcol] of [out_dim][W]
-          XS[xf + xoff(out_dim, W, j, kcol, 0)] = (uint16_t)(th[qq] >> 16);
-          XS[xf + xoff(out_dim, W, j, kcol, 1)] = (uint16_t)(tm[qq] >> 16);
-          XS[xf + xoff(out_dim, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
+          XS[xf + xoff(kOD, W, j, kcol, 0)] = (uint16_t)(th[qq] >> 16);
+          XS[xf + xoff(kOD, W, j, kcol, 1)] = (uint16_t)(tm[qq] >> 16);
+          XS[xf + xoff(kOD, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
 #endif
         }
         if (!G) {   // transposed copy: Mᵀ[kcol][j..j+3] is one 8-B run per plane
@@ -1645,9 +1651,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           const u2 vh = {pk_top(th[0], th[1]), pk_top(th[2], th[3])};
           const u2 vm = {pk_top(tm[0], tm[1]), pk_top(tm[2], tm[3])};
           const u2 vl = {pk_top(tl[0], tl[1]), pk_top(tl[2], tl[3])};
-          *reinterpret_cast<u2*>(XS + xb + xoff(W, out_dim, kcol, jb, 0)) = vh;
-          *reinterpret_cast<u2*>(XS + xb + xoff(W, out_dim, kcol, jb, 1)) = vm;
-          *reinterpret_cast<u2*>(XS + xb + xoff(W, out_dim, kcol, jb, 2)) = vl;
+          *reinterpret_cast<u2*>(XS + xb + xoff(W, kOD, kcol, jb, 0)) = vh;
+          *reinterpret_cast<u2*>(XS + xb + xoff(W, kOD, kcol, jb, 1)) = vm;
+          *reinterpret_cast<u2*>(XS + xb + xoff(W, kOD, kcol, jb, 2)) = vl;
         }
       }
     }
@@ -1721,7 +1727,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, 
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
     if constexpr (X3)
-      dw_tile_x3<C::T, C::TK, C::NW>(a, SZ + (int64_t)layer * WN, W,
+      dw_tile_x3<C::T, C::TK, C::NW, W, W>(a, SZ + (int64_t)layer * WN, W,
                                      SH + (int64_t)(layer - 1) * WN, W, (u / C::NTK) * C::T,
                                      (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
                                      pw + (int64_t)W * W, xs_mat(W, D, L, false, layer),
@@ -1736,7 +1742,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, 
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
     if constexpr (X3)
-      dw_tile_x3<C::TD, C::TK, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
+      dw_tile_x3<C::TD, C::TK, C::NW, W, D>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
                                       (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
                                       pw + (int64_t)W * D, xs_mat(W, D, L, false, L + 1),
                                       xs_mat(W, D, L, true, L + 1), D, (u % C::NTK) == 0,
