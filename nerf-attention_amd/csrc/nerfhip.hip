@@ -1788,10 +1788,12 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, 
 // Split-K second pass: g = Σ_split gpart[split][i] in split order (fixed, so
 // deterministic), then Adam on parameter i and, for weights, the transposed
 // copy.  One thread per canonical parameter index; grid (ceil(P/256), n_fits).
+// (W, D compile-time: the index splits and split-copy addresses fold to
+// shifts and multiplies)
+template <int W, int D>
 __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   const int fit = blockIdx.y;
   const int L = a.fit_layers[fit];
-  const int W = a.W, D = a.D;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n_params(W, D, L)) return;
   const float* g = a.gpart + fit * a.gp_stride + i;
@@ -2078,7 +2080,7 @@ int launch_params(const KArgs& a, hipStream_t st) {
                      st, a);
   if (a.n_split > 1) {
     const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
-    hipLaunchKernelGGL(k_adam_split, dim3(blocks, a.n_fits), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_adam_split<W, D>), dim3(blocks, a.n_fits), dim3(256), 0, st, a);
   }
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
