@@ -1048,7 +1048,10 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
 // ---------------------------------------------------------------------------
 constexpr unsigned kKsDynLds = 81920;   // bytes of LDS padding per K-split workgroup
 template <int W> struct KsCfg {
-  static constexpr int PD = W >= 512 ? 8 : 6;   // A-fragment items (S8) in flight per wave
+  // A-fragment items (S8) in flight per wave.  (W = 256: 10 and 12 items
+  // measured 3.5 % and 7 % slower than 6 on one medium fit: not load-latency
+  // bound, profiles/r02/ab_ks_prefetch_depth.log)
+  static constexpr int PD = W >= 512 ? 8 : 6;
 };
 __host__ __device__ constexpr int ks_owner(int J) { return (J >> 1) & 3; }
 __host__ __device__ constexpr int ks_local(int J) { return 2 * (J >> 3) + (J & 1); }
