@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--all-ranks", action="store_true")
     ap.add_argument("--partition", default="lpt")
+    ap.add_argument("--reverse", action="store_true", help="time the ranks last to first")
     args = ap.parse_args()
     plan, specs = sweep_280(2048, seed=0)
     costs = [engine.fit_flops(2048, 128, s.config, args.epochs) for s in specs]
@@ -35,7 +36,8 @@ def main():
     torch.cuda.synchronize()
     for n in [int(x) for x in args.worlds.split(",")]:
         times = []
-        for r in (range(n) if args.all_ranks else [0]):
+        ranks = list(range(n)) if args.all_ranks else [0]
+        for r in (ranks[::-1] if args.reverse else ranks):
             mine = farm.rank_share(costs, n, r, widths, args.partition)
             job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[0])
             torch.cuda.synchronize()
@@ -45,6 +47,8 @@ def main():
             times.append(time.perf_counter() - t0)
             del job
         t = max(times)
+        if args.reverse:
+            times = times[::-1]          # report in rank order
         print(json.dumps({"world": n, "partition": args.partition, "epochs": args.epochs, "rank_s": [round(x, 3) for x in times],
                           "pred_fits_per_s": round(280 / (t * 2000 / args.epochs), 2)}), flush=True)
 
