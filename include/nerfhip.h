@@ -141,7 +141,7 @@ int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const
 /* Per-kernel device time of a group, measured with hipEvents bracketing
  * every launch of its two step kernels (bench.py's roofline leg). */
 typedef struct nerfhip_timing {
-  int32_t launches;        /* out: timed launches per kernel (= the epochs)   */
+  int32_t launches;        /* out: timed launches per kernel (every 4th epoch) */
   int32_t reserved;
   double rows_ms;          /* out: Σ duration of the row-step launches        */
   double params_ms;        /* out: Σ duration of the parameter-step launches  */

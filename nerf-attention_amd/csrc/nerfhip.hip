@@ -2305,6 +2305,13 @@ GroupRun make_run(const nerfhip_group* g, void* stream) {
 
 }  // namespace
 
+// The timed variant brackets every kTimeStride-th epoch's two launches with
+// hipEvents (all of them measured 0.5 % of the sweep's wall clock, bench
+// --no-kernel-timing A/B, profiles/r02/bench_event_overhead.log); the
+// averages are over the timed launches.
+constexpr int kTimeStride = 4;
+static int timed_epochs(int E) { return (E + kTimeStride - 1) / kTimeStride; }
+
 static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* streams,
                     nerfhip_timing* timings) {
   if (!groups || !streams || n_groups < 1) return NERFHIP_ERR_NULL;
@@ -2324,8 +2331,9 @@ static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* 
     rc = select_device(groups[i].device, &cur);
     if (rc == NERFHIP_OK) rc = prologue(runs[i]);
     if (ev && rc == NERFHIP_OK) {
-      // 3 events per epoch: before the row step, between, after the param step
-      const int ne = 3 * groups[i].epochs;
+      // 3 events per timed epoch (every kTimeStride-th): before the row step,
+      // between, after the param step
+      const int ne = 3 * timed_epochs(groups[i].epochs);
       ev[i] = new hipEvent_t[ne > 0 ? ne : 1]();
       for (int k = 0; k < ne && rc == NERFHIP_OK; ++k)
         if (hipEventCreate(&ev[i][k]) != hipSuccess) rc = NERFHIP_ERR_LAUNCH;
@@ -2335,7 +2343,8 @@ static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* 
     for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
       if (e >= groups[i].epochs) continue;
       rc = select_device(groups[i].device, &cur);
-      if (rc == NERFHIP_OK) rc = epoch_step(runs[i], e, ev ? ev[i] + 3 * e : nullptr);
+      if (rc == NERFHIP_OK)
+        rc = epoch_step(runs[i], e, ev && e % kTimeStride == 0 ? ev[i] + 3 * (e / kTimeStride) : nullptr);
     }
   for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
     rc = select_device(groups[i].device, &cur);
@@ -2344,7 +2353,7 @@ static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* 
   if (ev) {
     for (int i = 0; i < n_groups; ++i) {
       if (!ev[i]) continue;
-      const int E = groups[i].epochs;
+      const int E = timed_epochs(groups[i].epochs);
       if (rc == NERFHIP_OK) rc = select_device(groups[i].device, &cur);
       if (rc == NERFHIP_OK && hipStreamSynchronize(runs[i].st) != hipSuccess) rc = NERFHIP_ERR_LAUNCH;
       if (rc == NERFHIP_OK) {
