@@ -2006,18 +2006,21 @@ int32_t split_for(const nerfhip_group* g, const nerfhip_sizes& s) {
 // fit 4x the waves and a quarter of the serial GEMM chain per wave, at 4x the
 // weight reads per row and one barrier per output tile: it pays only while the
 // regular kernel leaves most CUs idle, i.e. for groups whose regular grid
-// (n_fits · n_pad/64 workgroups) is below kKsMaxWorkgroups.  Measured (rows
-// kernel, bf16x3): one medium fit at 2048 (32 regular workgroups) 0.092 →
-// 0.067 ms; 8 medium fits 0.096 → 0.254; 5 large fits 0.29 → 0.62; one wide
-// fit at 8192 (128) 0.36 → 0.59.  NERFHIP_ROWS_KS = 0 / 1 forces the choice
+// (n_fits · n_pad/64 workgroups) is at most kKsMaxWorkgroups, so that the
+// K-split grid (4x) runs in one round at one workgroup per CU.  Measured (rows
+// kernel, bf16x3, medium): one fit at 1024 / 2048 / 4096 (16 / 32 / 64 regular
+// workgroups) 0.093 → 0.066 ms each; two fits at 2048 (64) 0.093 → 0.068;
+// three fits (96) 0.093 → 0.125; 8 fits 0.096 → 0.254; 5 large fits 0.29 →
+// 0.62; one wide fit at 8192 (128) 0.36 → 0.59; one large fit at 2048 (32)
+// 0.256 → 0.201 (profiles/r02/ks_threshold.log).  NERFHIP_ROWS_KS = 0 / 1 forces the choice
 // (supported shapes only: bf16x3, W >= 128, D = 128).
-constexpr int64_t kKsMaxWorkgroups = 48;
+constexpr int64_t kKsMaxWorkgroups = 64;
 bool rows_ks_for(const nerfhip_group* g, const nerfhip_sizes& s) {
   if (g->precision != NERFHIP_PRECISION_BF16X3 || g->W < 128 || g->D != 128) return false;
   const char* e = getenv("NERFHIP_ROWS_KS");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return (int64_t)g->n_fits * (s.n_pad / kRowPad) < kKsMaxWorkgroups;
+  return (int64_t)g->n_fits * (s.n_pad / kRowPad) <= kKsMaxWorkgroups;
 }
 
 KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
