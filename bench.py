@@ -16,14 +16,19 @@ to the same per-fit parity bar (cos_delta_vs_ref).  With --also-fp32 (default
 on at N=1) the line also carries one timed fp32 sweep.
 
 Also reported (rank 0):
-  roofline      the dominant kernel's algorithmic TFLOP/s (hipEvent-timed over
-                the timed steps, while the width groups run concurrently)
-                against the matrix-core peak of its arithmetic: 157.3 TFLOP/s
-                f32 MFMA, or 2.5 PFLOP/s bf16 dense / 6 products = 416.7
-                TFLOP/s fp32-equivalent for bf16x3; plus the same kernel timed
-                alone for 20 epochs after the timed region ("isolated");
-  cpu_baseline  the oracle (CPU restatement of the reference loop) timed on a
-                bounded sample of the same workload on this host (N=1 only);
+  roofline      the dominant kernel's algorithmic TFLOP/s against the
+                matrix-core peak of its arithmetic (157.3 TFLOP/s f32 MFMA, or
+                2.5 PFLOP/s bf16 dense / 6 products = 416.7 TFLOP/s
+                fp32-equivalent for bf16x3).  `frac` / `achieved` /
+                `avg_launch_ms` are the kernel on its heaviest group timed
+                alone (hipEvents, 40 epochs right after the timed region, the
+                cold first launch excluded); `frac_concurrent` is the same
+                kernel's launches inside the timed sweep, where ~7 group
+                streams share the GPU; `job_frac` is the whole sweep's
+                algorithmic rate;
+  cpu_baseline  the package's own host path (nerf_attention/host_fit.py: the
+                reference loop in eager PyTorch) timed on a bounded sample of
+                the same workload on this host's CPUs (N=1 only);
   cos_delta_vs_ref  per-fit |Δ final_cosine_mean| against the reference's own
                 seed-0 sweep (tests/golden/sweep_ref_seed0_e2000.json).
 """
@@ -38,8 +43,7 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
-for _p in (ROOT / "nerf-attention_amd", ROOT / "oracle"):
-    sys.path.insert(0, str(_p))
+sys.path.insert(0, str(ROOT / "nerf-attention_amd"))
 
 # one hardware queue per width-group stream (the engine runs ~7 streams per
 # GPU; HIP's default of 4 queues makes some of them share a queue, in order).
@@ -95,13 +99,16 @@ def host_cpus() -> dict:
             "threads": min(logical, quota) if quota else logical}
 
 
-def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 3) -> dict:
-    """Time the oracle (the reference's CPU loop, restated op for op) on every
-    architecture for `sample_epochs` epochs, `repeats` times, on every CPU this
-    process may use; the median per-epoch time of each architecture is
+def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
+                 warmup_epochs: int = 10) -> dict:
+    """Time the package's own host path (host_fit.fit_on_host: the reference
+    loop, siren.py:80-149, in eager PyTorch) on every architecture: one untimed
+    warm-up fit of `warmup_epochs` per architecture (thread pool, allocator,
+    first-touch), then `repeats` fits of `sample_epochs` epochs, on every CPU
+    this process may use.  The median per-epoch time of each architecture is
     extrapolated to the 280-fit sweep (dense cost is data-independent)."""
-    import siren_oracle
     from nerf_attention import CONFIGS_FULL, SIREN
+    from nerf_attention.host_fit import fit_on_host
     from nerf_attention.synthetic import kv_slice
     cpus = host_cpus()
     threads = cpus["threads"]
@@ -109,27 +116,35 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 3) -> dict:
     torch.set_num_threads(threads)
     keys, _ = kv_slice(16, 2, seq_len=seq_len)
     samples = {c.name: [] for c in CONFIGS_FULL}
+
+    def one(cfg, epochs):
+        torch.manual_seed(0)
+        m = SIREN(cfg, 128)
+        return fit_on_host(keys, cfg, m, epochs, 1e-4, 0).train_time_seconds / epochs
+
     try:
+        for cfg in CONFIGS_FULL:
+            one(cfg, warmup_epochs)
         for _ in range(repeats):
             for cfg in CONFIGS_FULL:
-                torch.manual_seed(0)
-                init = SIREN(cfg, 128).flat_parameters()
-                r = siren_oracle.fit(keys, cfg.hidden_features, cfg.hidden_layers, cfg.omega_0,
-                                     init, sample_epochs)
-                samples[cfg.name].append(r["train_time_seconds"] / sample_epochs)
+                samples[cfg.name].append(one(cfg, sample_epochs))
     finally:
         torch.set_num_threads(prev)
     per_epoch = {k: float(np.median(v)) for k, v in samples.items()}
     sweep_s = 40 * 2000 * sum(per_epoch.values())
-    spread = max(max(v) / min(v) for v in samples.values()) - 1.0
+    # spread of the repeats around the median, worst architecture
+    spread = max((max(v) - min(v)) / float(np.median(v)) for v in samples.values())
     return {"value": 280.0 / sweep_s, "unit": "fits/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/siren_oracle.py (the reference loop restated), each of the 7 archs "
-                      f"for {sample_epochs} epochs x {repeats} repeats on synthetic L16 H2 key "
-                      f"[{seq_len},128], median per-epoch time per arch; sweep = "
+            "port": "package host path (nerf_attention/host_fit.py)",
+            "sample": f"nerf_attention/host_fit.py (the reference loop in eager PyTorch), each of "
+                      f"the 7 archs: 1 untimed warm-up of {warmup_epochs} epochs, then "
+                      f"{repeats} repeats x {sample_epochs} epochs on synthetic L16 H2 key "
+                      f"[{seq_len},128]; median per-epoch time per arch; sweep = "
                       f"40x2000x(sum of medians) = {sweep_s:.0f}s; {cpus['model']}, "
                       f"{threads} torch threads (affinity {cpus['affinity_cpus']} CPUs, "
                       f"cgroup quota {cpus['cgroup_cpu_quota']})",
             "host": cpus, "repeat_spread": round(spread, 4),
+            "repeat_spread_kind": "(max - min) / median of the timed repeats, worst arch",
             "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()}}
 
 
@@ -160,9 +175,11 @@ def e2e_fit_kv_cache(seq_len: int, epochs: int, precision: str) -> dict:
             "note": "whole fit_kv_cache call incl. loads, inits, D2H, checkpoints and JSON"}
 
 
-def isolated_kernel(gspecs, kname, flops, precision, peak, device, epochs=20) -> dict:
+def isolated_kernel(gspecs, kname, flops, precision, peak, device, epochs=41) -> dict:
     """The dominant kernel's group trained alone (no concurrent groups) for a
-    few epochs, after the timed region: its undisturbed launch time."""
+    few epochs, after the timed region: its undisturbed launch time (every
+    4th epoch timed from epoch 3, so 10 launches at 41 epochs and never the
+    cold first one)."""
     from nerf_attention import engine
     job = engine.FitJob(gspecs, epochs, devices=[device], precision=precision)
     job.launch(timed=True)
@@ -171,7 +188,8 @@ def isolated_kernel(gspecs, kname, flops, precision, peak, device, epochs=20) ->
     ms = (t.rows_ms if "rows" in kname else t.params_ms) / t.launches
     tf = flops / (ms * 1e-3) / 1e12
     return {"avg_launch_ms": round(ms, 4), "achieved": round(tf, 2), "frac": round(tf / peak, 4),
-            "frac_of_f32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "epochs": epochs}
+            "frac_of_f32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "epochs": epochs,
+            "launches": t.launches}
 
 
 def fp32_sweep(specs, epochs, device, plan, ref_cos, n_total) -> dict:
@@ -228,7 +246,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--epochs", type=int, default=2000)
     ap.add_argument("--seq-len", type=int, default=2048)
-    ap.add_argument("--cpu-sample-epochs", type=int, default=150)
+    ap.add_argument("--cpu-sample-epochs", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"])
@@ -337,46 +355,53 @@ def main() -> None:
                 # PMC bytes per launch (separate, serialised rocprofv3 passes of the
                 # same workload, tools/profile_round.sh) over this run's launch time
                 hbm = traffic["bytes"] / (avg_ms * 1e-3) / 1e9
-            roof = {"bound": "mfma", "achieved": round(achieved, 3),
+            gcf = [specs[mine[i]].config for i in g.members]
+            g_flops = (rows_flops if "rows" in kname else params_flops)(N, 128, gcf)
+            iso = isolated_kernel([specs[mine[i]] for i in g.members], kname, g_flops,
+                                  args.precision, peak, local)
+            iso["fits"] = g.n
+            hbm_iso = traffic and traffic["bytes"] / (iso["avg_launch_ms"] * 1e-3) / 1e9
+            roof = {"bound": "mfma", "achieved": iso["achieved"],
                     "peak": round(peak, 1), "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4),
-                    "frac_kind": "dominant kernel, algorithmic FLOPs per launch / mean launch "
-                                 "duration in the timed region, where the width groups' "
-                                 "streams share the GPU (see isolated and job_frac)",
+                    "frac": iso["frac"],
+                    "frac_kind": "dominant kernel on its heaviest group, timed alone right after "
+                                 "the timed region: algorithmic FLOPs per launch / mean hipEvent "
+                                 "launch duration (10 launches, cold first launch excluded)",
+                    "avg_launch_ms": iso["avg_launch_ms"], "flops_per_launch": g_flops,
+                    "fits_per_launch": g.n,
                     "traffic": traffic and traffic["bytes"],
                     "traffic_detail": traffic,
                     "mfma_busy": traffic and traffic.get("mfma_busy"),
                     "mfma_busy_kind": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GPU-active "
-                                      "cycles), rocprofv3 PMC pass (dispatches serialised)",
-                    "hbm_gbs": hbm and round(hbm, 1),
-                    "hbm_frac": hbm and round(hbm / HBM_PEAK_GBS, 4),
+                                      "cycles), rocprofv3 PMC pass of the sweep (dispatches "
+                                      "serialised)",
+                    "hbm_gbs": hbm_iso and round(hbm_iso, 1),
+                    "hbm_frac": hbm_iso and round(hbm_iso / HBM_PEAK_GBS, 4),
                     "kernel": f"{kname} [{args.precision}]",
-                    "fits_per_launch": round(sum(x.n for x in job.groups
-                                                 if f"<{x.W}," in kname) /
-                                             sum(1 for x in job.groups if f"<{x.W}," in kname),
-                                             2),
-                    "avg_launch_ms": round(avg_ms, 4), "flops_per_launch": flops,
                     "flops_unit": "algorithmic fp32 GEMM FLOPs (2 per multiply-add), "
                                   "SURVEY.md §8d",
                     "peak_basis": ("f32 MFMA" if args.precision == "fp32" else
                                    "bf16 MFMA 2.5 PF dense / 6 bf16 products per fp32 product"),
-                    "note": "launch durations measured while the width groups run concurrently",
-                    "kernels_avg_ms": {k: round(v[0] / v[1], 4) for k, v in per_kernel.items()},
+                    "isolated": iso,
+                    "frac_concurrent": round(achieved / peak, 4),
+                    "concurrent": {
+                        "achieved": round(achieved, 3), "avg_launch_ms": round(avg_ms, 4),
+                        "flops_per_launch": flops,
+                        "fits_per_launch": round(sum(x.n for x in job.groups
+                                                     if f"<{x.W}," in kname) /
+                                                 sum(1 for x in job.groups if f"<{x.W}," in kname),
+                                                 2),
+                        "hbm_gbs": hbm and round(hbm, 1),
+                        "note": "the same kernel's launches inside the timed sweep (every 4th "
+                                "epoch), summed over every group of its width, while ~7 group "
+                                "streams share the GPU: a share of the chip, not a kernel "
+                                "property"},
+                    "kernels_avg_ms_concurrent": {k: round(v[0] / v[1], 4)
+                                                  for k, v in per_kernel.items()},
                     "groups": len(job.groups),
                     "job_achieved_tflops": round(job_tf, 2),
                     "job_frac": round(job_tf / peak, 4),
                     "job_frac_of_f32_mfma_peak": round(job_tf / FP32_MFMA_PEAK_TFLOPS, 4)}
-            if world == 1:
-                gcf = [specs[mine[i]].config for i in g.members]
-                g_flops = (rows_flops if "rows" in kname else params_flops)(N, 128, gcf)
-                roof["isolated"] = isolated_kernel(
-                    [specs[mine[i]] for i in g.members], kname, g_flops, args.precision, peak,
-                    local)
-                roof["isolated"]["fits"] = g.n
-                if traffic:
-                    hi = traffic["bytes"] / (roof["isolated"]["avg_launch_ms"] * 1e-3) / 1e9
-                    roof["isolated"]["hbm_gbs"] = round(hi, 1)
-                    roof["isolated"]["hbm_frac"] = round(hi / HBM_PEAK_GBS, 4)
         parity = None
         if GOLDEN_SWEEP.exists() and args.epochs == 2000 and args.seq_len == 2048:
             ref = json.loads(GOLDEN_SWEEP.read_text())["records"]

@@ -139,9 +139,10 @@ int nerfhip_group_sizes(int32_t W, int32_t D, int32_t N, int32_t L_max, int32_t 
 int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const* streams);
 
 /* Per-kernel device time of a group, measured with hipEvents bracketing
- * every launch of its two step kernels (bench.py's roofline leg). */
+ * the launches of its two step kernels in every 4th epoch (bench.py's
+ * roofline leg). */
 typedef struct nerfhip_timing {
-  int32_t launches;        /* out: timed launches per kernel (every 4th epoch) */
+  int32_t launches;        /* out: timed launches per kernel (epochs 3, 7, 11, ...: every 4th, never the cold first) */
   int32_t reserved;
   double rows_ms;          /* out: Σ duration of the row-step launches        */
   double params_ms;        /* out: Σ duration of the parameter-step launches  */

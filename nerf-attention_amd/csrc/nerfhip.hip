@@ -2311,9 +2311,12 @@ GroupRun make_run(const nerfhip_group* g, void* stream) {
 // The timed variant brackets every kTimeStride-th epoch's two launches with
 // hipEvents (all of them measured 0.5 % of the sweep's wall clock, bench
 // --no-kernel-timing A/B, profiles/r02/bench_event_overhead.log); the
-// averages are over the timed launches.
+// averages are over the timed launches.  The sampled epochs are
+// kTimeStride-1, 2·kTimeStride-1, …: the cold first launch (code-object load,
+// cold L2) is never among them.
 constexpr int kTimeStride = 4;
-static int timed_epochs(int E) { return (E + kTimeStride - 1) / kTimeStride; }
+static int timed_epochs(int E) { return E / kTimeStride; }
+static bool timed_epoch(int e) { return e % kTimeStride == kTimeStride - 1; }
 
 static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* streams,
                     nerfhip_timing* timings) {
@@ -2347,7 +2350,8 @@ static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* 
       if (e >= groups[i].epochs) continue;
       rc = select_device(groups[i].device, &cur);
       if (rc == NERFHIP_OK)
-        rc = epoch_step(runs[i], e, ev && e % kTimeStride == 0 ? ev[i] + 3 * (e / kTimeStride) : nullptr);
+        rc = epoch_step(runs[i], e, ev && timed_epoch(e) && e / kTimeStride < timed_epochs(groups[i].epochs)
+                                          ? ev[i] + 3 * (e / kTimeStride) : nullptr);
     }
   for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
     rc = select_device(groups[i].device, &cur);

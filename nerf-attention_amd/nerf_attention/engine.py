@@ -414,14 +414,20 @@ def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
 
 
 def fit_device_bytes(spec: FitSpec, epochs: int, log_every: int = 0, precision=None) -> int:
-    """Device bytes one fit occupies in a group (nerfhip_group_sizes buffers)."""
+    """Device bytes one fit occupies in a group (nerfhip_group_sizes buffers,
+    as _Group allocates them: params_init, params, adam_m, adam_v; params_t;
+    scratch; target, target_norm, eval_y; mean, std; loss partials; row_cos,
+    row_sq; the split-K slab (counted even when the group does not take it);
+    probes; the bf16x3 split copies; and, once per group but counted per fit,
+    the positions, the schedule table and the layer / omega vectors)."""
     N, D = int(spec.target.shape[0]), int(spec.target.shape[1])
     c = spec.config
     s = _native.group_sizes(c.hidden_features, D, N, c.hidden_layers, epochs)
     n_probe = epochs // log_every if log_every > 0 else 0
-    floats = (3 * s.params + s.params_t + s.scratch + 3 * s.target + 2 * s.stats
+    floats = (4 * s.params + s.params_t + s.scratch + 3 * s.target + 2 * s.stats
               + max(s.loss_partial, 1) + 2 * s.rows + s.grad_partial
-              + n_probe * (s.target + 2 * s.rows))
+              + n_probe * (s.target + 2 * s.rows)
+              + s.rows + 2 * max(epochs, 1) + 2)
     return 4 * int(floats) + (2 * int(s.wsplit) if check_precision(precision) == "bf16x3" else 0)
 
 

@@ -12,8 +12,9 @@ There is ONE multi-GPU design, used by every entry point:
     GPU and the ranks meet only at the gloo barrier / max / gather;
   * `fit_kv_cache(gpus=N)` / `run_fits(devices=[...])`: `run_farm` starts one
     worker process per device (fresh interpreters, started before this
-    process needs the GPU for anything), each worker trains its LPT share on
-    its device and sends the outputs back to the parent over a pipe.
+    process needs the GPU for anything), each worker trains its share
+    (rank_share under farm.auto_partition / NERFHIP_FARM_PARTITION) on its
+    device and sends the outputs back to the parent over a pipe.
 The reference loop being farmed is fit.py:54-86 (strictly sequential there).
 """
 
@@ -204,7 +205,9 @@ def _farm_worker(device: int, jobs: list, epochs: int, lr: float, log_every: int
 def run_farm(specs: list, epochs: int, devices: list, lr: float = 1e-4, log_every: int = 0,
              precision=None, timeout: float | None = None) -> list:
     """Train `specs` over `devices`, one worker process per device, each on its
-    LPT share (rank_share on the FLOP model).  Returns FitOutput per spec, in
+    share: rank_share on the FLOP model with the partition auto_partition picks
+    for this device count (width-blocked at 2, LPT from 4) or
+    NERFHIP_FARM_PARTITION names.  Returns FitOutput per spec, in
     spec order, with `params` on the host and `device` naming where it
     trained.  Per-fit arithmetic does not depend on the device count beyond
     the engine's own group sizing (see engine.SPLIT_MAX_FITS)."""

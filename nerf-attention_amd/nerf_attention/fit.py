@@ -288,10 +288,17 @@ def main() -> None:
                         help='GEMM arithmetic (extension; default bf16x3 = exact 3-way bf16 '
                              'split, fp32-class; fp32 = f32 MFMA)')
     args = parser.parse_args()
+    # The reference's CLI falls back to the CPU when no GPU is present
+    # (fit.py:192-194).  The CPU run is this package's explicit host path
+    # (host_fit.py: eager PyTorch, the reference arithmetic); a HIP request made
+    # through the Python API (fit_siren / fit_kv_cache with device='cuda') still
+    # raises on such a host.  device_count() counts without initialising HIP,
+    # so a later --gpus farm can still start its workers cleanly.
+    if args.device == 'cuda' and torch.cuda.device_count() == 0:
+        print("CUDA not available, falling back to CPU")
+        args.device = 'cpu'
     if args.seed is not None:
         torch.manual_seed(args.seed)
-    # The reference falls back to CPU when CUDA is missing (fit.py:192-194);
-    # this engine has no CPU path, so resolve_device raises instead.
     t0 = time.time()
     fit_kv_cache(Path(args.kv_dir), Path(args.output_dir), args.epochs, args.device,
                  args.quick, gpus=args.gpus, select=args.select,

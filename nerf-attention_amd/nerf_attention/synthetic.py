@@ -47,6 +47,17 @@ def _threads() -> int:
 POOL_MIN_ROWS = 32 * 4096     # slices x seq_len below which one process is faster
 
 
+
+def _hip_untouched() -> bool:
+    """True while nothing in this process can have created HIP runtime state:
+    torch has not initialised its HIP context and the engine library
+    (libnerfhip, whose calls initialise HIP on their own) is not loaded.
+    Only then may the generator fork its workers; otherwise it spawns fresh
+    interpreters.  (torch.cuda.device_count() on ROCm counts through amdsmi
+    and does not initialise HIP.)"""
+    from . import _native
+    return _native._lib is None and not torch.cuda.is_initialized()
+
 def kv_slices(pairs, seq_len: int = 2048, num_layers: int = 32, num_kv_heads: int = 8,
               head_dim: int = 128) -> list:
     """kv_slice for every (layer, head) in `pairs`.  Large requests run on a
@@ -67,7 +78,7 @@ def kv_slices(pairs, seq_len: int = 2048, num_layers: int = 32, num_kv_heads: in
     nbytes = int(np.prod(shape)) * 4
     jobs = [(k, l, h) for k, (l, h) in enumerate(pairs)]
     parts = [jobs[w::workers] for w in range(workers)]
-    if not torch.cuda.is_initialized():
+    if _hip_untouched():
         # fork: the workers inherit an anonymous shared mapping and write the
         # slices straight into it; the result is a view of it (no copy)
         mm = mmap.mmap(-1, nbytes, flags=mmap.MAP_SHARED)

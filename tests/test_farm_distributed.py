@@ -90,24 +90,26 @@ def _bench_env(**extra):
     return env
 
 
-def test_bench_spawns_ranks_for_gpus_2():
-    """`python bench.py --gpus 2` without a launcher starts two ranks itself;
-    they form a gloo group, split the 280 fits by LPT and meet in the barrier,
-    max and gather; rank 0 prints one line that saw both ranks."""
-    r = _sp.run([_sys.executable, str(_BENCH), "--gpus", "2", "--dry-run"], env=_bench_env(),
-                capture_output=True, text=True, timeout=300)
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_spawns_ranks(world):
+    """`python bench.py --gpus N` without a launcher starts N ranks itself
+    (N = 8 is the driver's full-node case); they form a gloo group, split the
+    280 fits (farm.auto_partition: width-blocked at 2, LPT at 8) and meet in
+    the barrier, max and gather; rank 0 prints one line that saw every rank."""
+    r = _sp.run([_sys.executable, str(_BENCH), "--gpus", str(world), "--dry-run"],
+                env=_bench_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     line = _json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2
-    assert line["fits"] == list(range(280)) and set(line["owner"]) == {0, 1}
+    assert line["n_gpus"] == world and line["ranks_seen"] == world
+    assert line["fits"] == list(range(280)) and set(line["owner"]) == set(range(world))
     costs = _costs()
     widths = [c.hidden_features for c in CONFIGS_FULL] * 40
-    assert [farm.rank_share(costs, 2, k, widths) for k in (0, 1)] == \
-        [[i for i, o in enumerate(line["owner"]) if o == k] for k in (0, 1)]
-    lo, hi = sorted(line["rank_flops"])
-    assert hi / lo < 1.05
+    assert [farm.rank_share(costs, world, k, widths) for k in range(world)] == \
+        [[i for i, o in enumerate(line["owner"]) if o == k] for k in range(world)]
+    loads = line["rank_flops"]
+    assert max(loads) / min(loads) < 1.05
 
 
 def test_partitions_cover_and_balance():

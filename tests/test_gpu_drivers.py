@@ -237,3 +237,21 @@ def test_latency_harness(gpu, tmp_path, capsys):
         assert re.fullmatch(rf"  {r['name']}: SIREN=\d+\.\d{{3}}ms \| HBM\(4060\)=\d+\.\d{{3}}ms \| "
                             rf"HBM\(H100\)=\d+\.\d{{3}}ms", line)
     assert 0 < profile_siren_latency(tmp_path / "fits", 512, "cuda") < 50
+
+
+def test_fit_device_bytes_covers_group_buffers(gpu):
+    """engine.fit_device_bytes (the memory-wave planner's per-fit size) is at
+    least what a real one-fit group allocates, buffer by buffer."""
+    from nerf_attention.synthetic import kv_slice
+    keys, _ = kv_slice(0, 0, seq_len=512)
+    for cfg, prec in ((SIRENConfig(256, 2, 30.0, "medium"), "bf16x3"),
+                      (SIRENConfig(64, 1, 30.0, "tiny"), "fp32")):
+        torch.manual_seed(0)
+        spec = engine.FitSpec(target=keys, config=cfg, init=SIREN(cfg, 128).flat_parameters())
+        job = engine.FitJob([spec], 20, log_every=5, devices=[0], precision=prec)
+        g = job.groups[0]
+        held = sum(t.numel() * t.element_size() for t in vars(g).values()
+                   if isinstance(t, torch.Tensor) and t.device.type == "cuda")
+        need = engine.fit_device_bytes(spec, 20, 5, prec)
+        assert need >= held, (cfg.name, need, held)
+        assert need <= 1.3 * held + (1 << 20), (cfg.name, need, held)

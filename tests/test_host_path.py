@@ -145,3 +145,63 @@ def test_latency_harness_cpu(tmp_path):
     _save_model(tmp_path, "L0_H0_key_tiny", r, _result_to_record("L0_H0_key_tiny", 0, 0, "key", r))
     recs = profile_latency(tmp_path, tmp_path / "lat", device="cpu")
     assert len(recs) == 1 and recs[0]["num_params"] == 12608 and recs[0]["siren_time_ms"] > 0
+
+
+def test_fit_cli_falls_back_to_cpu(tmp_path, golden_dir):
+    """`python -m nerf_attention.fit --quick` on a host without a GPU prints
+    the reference's fallback line and runs the package's host path
+    (reference fit.py:192-194), with the reference quick run's records and
+    stdout structure (schema_quick/)."""
+    import os
+    import re
+    import subprocess
+    import sys
+    from pathlib import Path
+    from nerf_attention.synthetic import extract_kv_cache_synthetic
+    root = Path(__file__).resolve().parent.parent
+    kv = tmp_path / "kv"
+    extract_kv_cache_synthetic(seq_len=512, num_layers=4, num_kv_heads=4, head_dim=128,
+                               output_dir=kv)
+    env = dict(os.environ, PYTHONPATH=str(root / "nerf-attention_amd"),
+               HIP_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    r = subprocess.run([sys.executable, "-m", "nerf_attention.fit", "--kv_dir", str(kv),
+                        "--output_dir", str(tmp_path / "fits"), "--epochs", "20", "--quick",
+                        "--seed", "0"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    num = re.compile(r"-?\d+\.\d+")
+    shape = lambda t: [num.sub("#", l) for l in t.splitlines()]  # noqa: E731
+    ref_out = (golden_dir / "schema_quick" / "stdout.txt").read_text()
+    lines = shape(r.stdout)
+    assert lines[0] == "CUDA not available, falling back to CPU"
+    assert lines[1:-1] == shape(ref_out) + [""] and "sweep wall clock" in lines[-1]
+    recs = json.loads((tmp_path / "fits" / "fit_results.json").read_text())
+    ref = json.loads((golden_dir / "schema_quick" / "fit_results.json").read_text())
+    assert [list(a) for a in recs] == [list(b) for b in ref]
+    for a, b in zip(recs, ref):
+        assert a["name"] == b["name"] and a["num_parameters"] == b["num_parameters"]
+        assert abs(a["final_cosine_mean"] - b["final_cosine_mean"]) <= COS_TOL, a["name"]
+    assert len(list((tmp_path / "fits").glob("*_model.pt"))) == 6
+
+
+def test_bench_cpu_baseline_times_host_path():
+    """bench.py's cpu_baseline leg times the package's host path
+    (host_fit.fit_on_host) and never imports anything under oracle/."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    code = (
+        "import json, sys\n"
+        f"sys.path.insert(0, {str(root)!r})\n"
+        "import bench\n"
+        "r = bench.cpu_baseline(64, 2, repeats=2, warmup_epochs=1)\n"
+        f"bad = [m for m, v in list(sys.modules.items()) if {str(root / 'oracle')!r} in "
+        "str(getattr(v, '__file__', '') or '')]\n"
+        "print(json.dumps({'bad': bad, 'kind': r['kind'], 'port': r['port'], "
+        "'value': r['value'], 'archs': len(r['per_epoch_ms'])}))\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["bad"] == [] and out["kind"] == "port" and "host_fit" in out["port"]
+    assert out["value"] > 0 and out["archs"] == 7
