@@ -1057,9 +1057,33 @@ __host__ __device__ constexpr int ks_owner(int J) { return (J >> 1) & 3; }
 __host__ __device__ constexpr int ks_local(int J) { return 2 * (J >> 3) + (J & 1); }
 
 __device__ __forceinline__ void ks_barrier() {
+#ifdef NERFHIP_EXP_KS_VMWAIT   // diagnostic: also drain vector memory
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+
+// A phase's bias vector (n floats, n % 4 == 0) global → LDS.  Diagnostic
+// builds vary how (NERFHIP_EXP_KS_STAGE32: dword stores; _STAGE_ALL: every
+// wave writes the whole vector; _STAGE_BAR: a barrier right after).
+__device__ __forceinline__ void ks_stage(float* dst, const float* src, int n, int tid) {
+#if defined(NERFHIP_EXP_KS_STAGE32)
+  if (4 * tid < n) {
+    const f4 v = ld4(src + 4 * tid);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[4 * tid + q] = v[q];
+  }
+#elif defined(NERFHIP_EXP_KS_STAGE_ALL)
+  const int l = tid & 63;
+  for (int i = 4 * l; i < n; i += 256) st4(dst + i, ld4(src + i));
+#else
+  stage_vec(dst, src, n, tid);
+#endif
+#ifdef NERFHIP_EXP_KS_STAGE_BAR
+  ks_barrier();
+#endif
 }
 
 // A-fragment item i of a K-deep phase (tile J = i / NM, this wave's k-slice
@@ -1164,7 +1188,7 @@ __device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ src, const 
   owner_read(JT - 1);
 }
 
-template <int W, int D>
+template <int W, int D, int MODE>
 __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   static_assert(W >= 128 && D == 128, "K-split rows: W >= 128, D = 128");
   constexpr int JW = W / 16, JD = D / 16, PD = KsCfg<W>::PD;
@@ -1184,7 +1208,17 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   const bool valid = r < a.N;
   // one instantiation for both modes: the forward-only mode (a.mode = 1) runs
   // the same code with the stores and the backward skipped (see launch_rows)
-  const bool train = a.mode == 0;
+  // MODE -1: one instantiation, mode read at run time; 0 / 1: compile-time
+  // train / forward-only (diagnostic builds, NERFHIP_EXP_KS_MODES)
+  const bool train = MODE < 0 ? a.mode == 0 : MODE == 0;
+  // diagnostic builds: the mode compile-time in one part of the kernel only
+#if defined(NERFHIP_EXP_KS_SPLIT_H)
+  const bool train_h = train, train_f = a.mode == 0;
+#elif defined(NERFHIP_EXP_KS_SPLIT_F)
+  const bool train_h = a.mode == 0, train_f = train;
+#else
+  const bool train_h = train, train_f = train;
+#endif
   const int n_pad = a.n_pad;
   const float* P = a.params + fit * a.p_stride;
   float* S = a.scratch + fit * a.s_stride;
@@ -1215,7 +1249,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   ks_prefetch<W>(ring, XS + xs_mat(W, D, L, false, 1), c, g, w);
 
   // ---- layer 0 (K = 1, VALU): this wave's tiles J = 2s + h, s = w + 4m
-  stage_vec(bias, P, 2 * W, tid);
+  ks_stage(bias, P, 2 * W, tid);
   __syncthreads();
   const float x = a.pos[r];
   float* SHt = SH + (int64_t)rblk * W * 16 + g * 64 + (c & 3) * 16 + (c >> 2) * 4;
@@ -1230,7 +1264,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
       sincos_fast(__fmul_rn(om, z), &s, &co);
       ho[t][q] = s;
     }
-    if (train) {
+    if (train_h) {
       const f4 v = {ho[t][0], ho[t][1], ho[t][2], ho[t][3]};
       sst4(SHt + J * 256, quad_transpose(v, c));
     }
@@ -1240,7 +1274,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 
   // ---- hidden SineLayers 1..L
   for (int i = 1; i <= L; ++i) {
-    stage_vec(bias, P + off_hidden_w(W, i) + W * W, W, tid);
+    ks_stage(bias, P + off_hidden_w(W, i) + W * W, W, tid);
     float* SHi = SH + (int64_t)i * WN + eoff;
     float* SCi = SC + (int64_t)i * WN + coff;
     gemm_ks<W, JW, PD, W>(
@@ -1250,7 +1284,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
           const float z = __fadd_rn(acc, bias[16 * J + fe]);
           float s, co;
           sincos_fast(__fmul_rn(om, z), &s, &co);
-          if (train) {
+          if (train_h) {
             sst(SHi + J * 256, s);
             sst(SCi + J * 256, co);
           }
@@ -1261,21 +1295,21 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   }
 
   // ---- final nn.Linear(W, D), MSE, dL/dŷ
-  stage_vec(bias, P + off_final_w(W, L) + W * D, D, tid);
+  ks_stage(bias, P + off_final_w(W, L) + W * D, D, tid);
   const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + fe;
   float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + fe : nullptr;
   float* SGe = SG + (int64_t)rblk * D * 16 + fe * 16 + c;
   float sq = 0.f;
   gemm_ks<W, JD, PD, D>(
-      XS + xs_mat(W, D, L, false, L + 1), hs, ring, train ? XS + xs_mat(W, D, L, true, L + 1) : nullptr,
+      XS + xs_mat(W, D, L, false, L + 1), hs, ring, train_f ? XS + xs_mat(W, D, L, true, L + 1) : nullptr,
       w, c, g,
       lane, part, outb,
-      [&](int J) { return train ? T[16 * J] : 0.f; },
+      [&](int J) { return train_f ? T[16 * J] : 0.f; },
       [&](int J, float acc, float t) {
         const float y = __fadd_rn(acc, bias[16 * J + fe]);
         if (yo) yo[16 * J] = y;
         float gv = 0.f;
-        if (train) {
+        if (train_f) {
           const float diff = y - t;
           sq = valid ? fmaf(diff, diff, sq) : sq;
           gv = valid ? a.grad_scale * diff : 0.f;
@@ -1284,7 +1318,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
         return gv;
       },
       own);
-  if (!train) return;
+  if (!train_f) return;
   sq = wave_sum(sq);
   if (lane == 0) lsum[w] = sq;
   ys[0] = split_pair(ho[0], ho[1]);
@@ -1309,7 +1343,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   for (int i = L; i >= 2; --i)
     bwd(XS + xs_mat(W, D, L, true, i), hs, i - 1, XS + xs_mat(W, D, L, true, i - 1));
   // layer 0: cos(ω(x·w0 + b0)) recomputed; dZ0 reduced over the 16 rows at once
-  stage_vec(bias, P, 2 * W, tid);
+  ks_stage(bias, P, 2 * W, tid);
   float* PZ = SZ + (int64_t)rblk * 2 * W;
   gemm_ks<W, JW, PD, 0>(
       XS + xs_mat(W, D, L, true, 1), hs, ring, nullptr, w, c, g, lane, part, outb, no_pre,
@@ -1350,6 +1384,36 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kFs = 20;  // LDS floats per feature per 16-row block (16 + pad)
 
+// Staging slot of thread-round index i (feature·4 + quarter, quarter = 4 rows
+// of the 16-row block): a permutation inside every aligned group of 64 (one
+// wave's round = 16 features × 4 quarters) that decides which feature each
+// lane carries, so that the lane groups of the LDS store hit every bank once.
+// Global loads stay whole 128-B lines (the wave still reads one contiguous
+// 1 KB run); the LDS image, and so every result, is unchanged.
+//   bf16x3 (ds_write_b64, 16-lane groups, 48-B feature stride): a group holds
+//     features {0,2,4,6}, {1,3,5,7}, {8,10,12,14} or {9,11,13,15} — dword
+//     starts 12f mod 32 = 0/24/16/8 (or 12/4/28/20), 8 dwords each.  The
+//     identity (4 consecutive features per group) put two lanes on each of 8
+//     banks: 33 % of the kernel's LDS-array cycles were conflict cycles
+//     (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r02/pmc_isolated_groups.json).
+//   fp32 (ds_write_b128, 8-lane groups, 80-B feature stride): a group holds
+//     features {f, f+4}: dword starts 20f mod 32 and 20f + 16.
+template <bool X3> __device__ __forceinline__ int stage_slot(int i) {
+#ifdef NERFHIP_EXP_STAGE_IDENTITY   // diagnostic build: the round-2 (conflicted) lane order
+  return i;
+#endif
+  const int l = i & 63;
+  int f;
+  if constexpr (X3) {
+    const int g4 = l >> 4;
+    f = (g4 >> 1) * 8 + 2 * ((l >> 2) & 3) + (g4 & 1);
+  } else {
+    const int g8 = l >> 3;
+    f = (g8 >> 2) * 8 + (g8 & 3) + 4 * ((l >> 2) & 1);
+  }
+  return (i & ~63) | (f << 2) | (l & 3);
+}
+
 template <int TJ, int TK, int NW>
 __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict__ A, int FA,
                                         const float* __restrict__ B, int FB, int j0, int k0,
@@ -1377,17 +1441,19 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
       const int i = tid + NTH * m;      // m < TJ*4/NTH reads A, the rest B: uniform per m
+      const int sl = stage_slot<false>(i);
       if (m < TJ * 4 / NTH)
-        st[m] = ld4(Ab + rb * sA + i * 4);
+        st[m] = ld4(Ab + rb * sA + sl * 4);
       else if (NF4 % NTH == 0 || i < NF4)
-        st[m] = ld4(Bb + rb * sB + (i - TJ * 4) * 4);
+        st[m] = ld4(Bb + rb * sB + (sl - TJ * 4) * 4);
     }
   };
   auto lstore = [&](const f4 (&st)[NPT], float* buf) {
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
-      const int i = tid + NTH * m;           // feature i/4, quarter i%4 (A then B)
-      if (NF4 % NTH == 0 || i < NF4) st4(buf + (i >> 2) * kFs + (i & 3) * 4, st[m]);
+      const int i = tid + NTH * m;
+      const int sl = stage_slot<false>(i);   // feature sl/4, quarter sl%4 (A then B)
+      if (NF4 % NTH == 0 || i < NF4) st4(buf + (sl >> 2) * kFs + (sl & 3) * 4, st[m]);
     }
   };
 
@@ -1494,12 +1560,13 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   }
 }
 
-// bf16x3 form of dw_tile.  Each staged f4 (feature i/4, rows 4(i%4)..+3 of a
-// 16-row block) is split once, at the LDS store, into three bf16 planes
-// [3][TJ+TK features][kFx] (48-B feature stride: every ds_read_b128 lane
-// group covers a bank row once; the ds_write_b64 stores stay 2-way
-// conflicted — layouts that free both, e.g. 32-B features plus 16 B of pad
-// per 16, measured 8-10 % slower); a lane then reads its 8 rows of a feature
+// bf16x3 form of dw_tile.  Each staged f4 (feature s/4, rows 4(s%4)..+3 of a
+// 16-row block, s = stage_slot(i)) is split once, at the LDS store, into three
+// bf16 planes [3][TJ+TK features][kFx] (48-B feature stride: every
+// ds_read_b128 lane group covers a bank row once, and with stage_slot's lane
+// order every 16-lane ds_write_b64 group too; a layout change that freed both,
+// 32-B features plus 16 B of pad per 16, measured 8-10 % slower in round 2:
+// more LDS bytes per block); a lane then reads its 8 rows of a feature
 // as one 16-B slice per plane, and each (x, y) sub-tile takes six
 // v_mfma_f32_32x32x16_bf16 per 16-row block (hi and correction accumulators)
 // instead of eight v_mfma_f32_32x32x2_f32.  Bias sums come from the fp32
@@ -1538,14 +1605,16 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
 #pragma unroll
   for (int m = 0; m < NPA; ++m) bpart[m] = 0.f;
 
+  static_assert(NA4 % 64 == 0, "A rows must fill whole waves (stage_slot permutes within 64)");
   auto gload = [&](f4 (&st)[NPT], int rb) {
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
       const int i = tid + NTH * m;
+      const int so = stage_slot<true>(i);
       if (NA4 % NTH == 0 ? m < NPA : i < NA4)   // wave-uniform (NA4 % 64 == 0)
-        st[m] = ld4(Ab + rb * sA + i * 4);
+        st[m] = ld4(Ab + rb * sA + so * 4);
       else if (NF4 % NTH == 0 || i < NF4)
-        st[m] = ld4(Bb + rb * sB + (i - TJ * 4) * 4);
+        st[m] = ld4(Bb + rb * sB + (so - TJ * 4) * 4);
     }
   };
   auto lstore = [&](const f4 (&st)[NPT], uint16_t* buf, bool count) {
@@ -1557,7 +1626,8 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
         uint32_t sh[4], sm[4], sl[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) split3(v[s], sh[s], sm[s], sl[s]);
-        uint16_t* d = buf + (i >> 2) * kFx + (i & 3) * 4;
+        const int so = stage_slot<true>(i);
+        uint16_t* d = buf + (so >> 2) * kFx + (so & 3) * 4;
         const u2 vh = {pk_top(sh[0], sh[1]), pk_top(sh[2], sh[3])};
         const u2 vm = {pk_top(sm[0], sm[1]), pk_top(sm[2], sm[3])};
         const u2 vl = {pk_top(sl[0], sl[1]), pk_top(sl[2], sl[3])};
@@ -1667,7 +1737,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       if ((tid & 3) == 0 && tid + NTH * m < NA4) {
-        const int64_t idx = pb + j0 + ((tid + NTH * m) >> 2);
+        const int64_t idx = pb + j0 + (stage_slot<true>(tid + NTH * m) >> 2);
         if (G) {
           G[idx] = s;
         } else {
@@ -2065,7 +2135,14 @@ int launch_rows(const KArgs& a, hipStream_t st) {
       // under the CU count and the padding costs nothing.
       const char* e = getenv("NERFHIP_KS_DYN_LDS");
       const unsigned dyn = e ? (unsigned)atoi(e) : kKsDynLds;
-      hipLaunchKernelGGL((k_step_rows_ks<W, D>), dim3(grid), dim3(256), dyn, st, a);
+#ifdef NERFHIP_EXP_KS_MODES
+      if (a.mode == 0)
+        hipLaunchKernelGGL((k_step_rows_ks<W, D, 0>), dim3(grid), dim3(256), dyn, st, a);
+      else
+        hipLaunchKernelGGL((k_step_rows_ks<W, D, 1>), dim3(grid), dim3(256), dyn, st, a);
+#else
+      hipLaunchKernelGGL((k_step_rows_ks<W, D, -1>), dim3(grid), dim3(256), dyn, st, a);
+#endif
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
