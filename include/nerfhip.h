@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NERFHIP_ABI_VERSION 3
+#define NERFHIP_ABI_VERSION 4
 
 typedef enum nerfhip_status {
   NERFHIP_OK = 0,
@@ -157,6 +157,25 @@ int nerfhip_siren_fit_timed(const nerfhip_group* groups, int32_t n_groups,
 /* Forward only with the current params → eval_y (+ row metrics when
  * target/mean/std/row_cos/row_sq are set).  SIREN.forward, siren.py:60-61. */
 int nerfhip_siren_forward(const nerfhip_group* g, void* stream);
+
+/* How nerfhip_siren_fit will run a group's epoch (no device work; reads only
+ * the group's shape fields, precision and whether grad_partial is set). */
+typedef enum nerfhip_rows_variant {
+  NERFHIP_ROWS_REGULAR = 0,   /* k_step_rows: 64-row workgroups, one wave per 16 rows     */
+  NERFHIP_ROWS_KSPLIT = 1     /* k_step_rows_ks: four waves split every GEMM's k over one
+                                 16-row block (small bf16x3 groups, W >= 128, D = 128)   */
+} nerfhip_rows_variant;
+
+typedef struct nerfhip_plan {
+  int32_t rows_variant;       /* nerfhip_rows_variant                                    */
+  int32_t grad_split;         /* row slices of the weight-gradient reduction (1 = fused) */
+  int32_t rows_workgroups;    /* grid of the row step                                    */
+  int32_t params_workgroups;  /* grid of the parameter step                              */
+  int32_t launches_per_epoch; /* kernels enqueued per epoch                              */
+  int32_t reserved;
+} nerfhip_plan;
+
+int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out);
 
 /* ------------------------------------------------------------------------
  * Truncated-SVD baseline (BASELINE config 5).

@@ -2126,15 +2126,19 @@ int launch_rows(const KArgs& a, hipStream_t st) {
     if (a.rows_ks) {
       const int grid = grid_for(a.n_fits, a.n_pad / 16);
       // One K-split workgroup per CU: dynamic LDS padding keeps a second one
-      // off the CU.  A separate forward-only instantiation (TRAIN = false)
-      // gave wrong rows in ~5 % of the workgroups that shared a CU with
-      // another one (seq 8192, reproducible; gone with 96 KB of padding, not
-      // with 4 KB); the single runtime-mode kernel measured correct with and
-      // without sharing (tools/ks_diag4.py).  The cause was not isolated, so
-      // the kernel keeps a CU to itself; below kKsMaxWorkgroups the grid is
-      // under the CU count and the padding costs nothing.
-      const char* e = getenv("NERFHIP_KS_DYN_LDS");
-      const unsigned dyn = e ? (unsigned)atoi(e) : kKsDynLds;
+      // off the CU.  A separate forward-only instantiation (MODE = 1, diagnostic
+      // builds only) gave wrong rows in ~1-2 % of the workgroups that shared a
+      // CU with another one (profiles/r03/ks_coresidency.log: the trigger is the
+      // compile-time forward-only FINAL phase, and all four waves' partials of
+      // every final tile are wrong in a bad block); this single runtime-mode
+      // kernel measured correct with and without sharing, and
+      // tests/test_gpu_parity.py::test_rows_ks_coresident pins that.  The
+      // cause was not isolated, so the kernel keeps a CU to itself; below
+      // kKsMaxWorkgroups the grid is under the CU count and the padding costs
+      // nothing.  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics only) drops the
+      // padding so that two workgroups may share a CU.
+      const char* e = getenv("NERFHIP_KS_SHARE_CU");
+      const unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;
 #ifdef NERFHIP_EXP_KS_MODES
       if (a.mode == 0)
         hipLaunchKernelGGL((k_step_rows_ks<W, D, 0>), dim3(grid), dim3(256), dyn, st, a);
@@ -2490,6 +2494,26 @@ int nerfhip_siren_forward(const nerfhip_group* g, void* stream) {
   if (rc == NERFHIP_OK && g->target && g->mean && g->std && g->row_cos && g->row_sq)
     rc = row_metrics(r.a, g->eval_y, r.s.target, g->row_cos, g->row_sq, r.s.rows, r.st);
   return rc;
+}
+
+int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out) {
+  if (!g || !out) return NERFHIP_ERR_NULL;
+  int rc = validate(g->W, g->D, g->N, g->L_max, g->epochs);
+  if (rc != NERFHIP_OK) return rc;
+  if (g->n_fits < 1) return NERFHIP_ERR_BAD_SHAPE;
+  if (g->precision != NERFHIP_PRECISION_FP32 && g->precision != NERFHIP_PRECISION_BF16X3)
+    return NERFHIP_ERR_BAD_PRECISION;
+  nerfhip_sizes s;
+  fill_sizes(g->W, g->D, g->N, g->L_max, g->epochs, &s);
+  const KArgs a = make_args(g, s);
+  const int rows_per_wg = a.rows_ks ? 16 : 64;
+  out->rows_variant = a.rows_ks ? NERFHIP_ROWS_KSPLIT : NERFHIP_ROWS_REGULAR;
+  out->grad_split = a.n_split;
+  out->rows_workgroups = grid_for(a.n_fits, (int)(s.n_pad / rows_per_wg));
+  out->params_workgroups = grid_for(a.n_fits, (int)param_tiles(g->W, g->D, g->L_max) * a.n_split);
+  out->launches_per_epoch = a.n_split > 1 ? 3 : 2;
+  out->reserved = 0;
+  return NERFHIP_OK;
 }
 
 }  // extern "C"

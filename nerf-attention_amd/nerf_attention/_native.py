@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 from ._build import LIB
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # nerfhip_precision (include/nerfhip.h)
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
@@ -75,6 +75,13 @@ class NerfhipTiming(ctypes.Structure):
                 ("params_ms", ctypes.c_double)]
 
 
+class NerfhipPlan(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("rows_variant", "grad_split", "rows_workgroups",
+                                        "params_workgroups", "launches_per_epoch", "reserved")]
+
+
+ROWS_VARIANTS = {0: "regular", 1: "ksplit"}   # nerfhip_rows_variant
+
 # every symbol include/nerfhip.h declares, with its ctypes signature
 SIGNATURES = {
     "nerfhip_abi_version": (c_int32, []),
@@ -85,6 +92,7 @@ SIGNATURES = {
     "nerfhip_siren_fit_timed": (c_int32, [POINTER(NerfhipGroup), c_int32, POINTER(c_void_p),
                                           POINTER(NerfhipTiming)]),
     "nerfhip_siren_forward": (c_int32, [POINTER(NerfhipGroup), c_void_p]),
+    "nerfhip_group_plan": (c_int32, [POINTER(NerfhipGroup), POINTER(NerfhipPlan)]),
     "nerfhip_svd_rank_metrics": (c_int32, [POINTER(NerfhipSvdBatch), c_void_p]),
     "nerfhip_kv_analysis": (c_int32, [POINTER(NerfhipKvAnalysisBatch), c_void_p]),
 }

@@ -62,6 +62,7 @@ class FitOutput:
     flop_share_seconds: float = 0.0   # group time x this fit's share of its FLOPs
     group_seconds: float = 0.0
     device: int = 0
+    plan: dict = field(default_factory=dict)   # how its group ran (_Group.plan)
 
 
 def fit_flops(seq_len: int, d_head: int, cfg: SIRENConfig, epochs: int) -> float:
@@ -235,6 +236,16 @@ class _Group:
             self.ev_start = torch.cuda.Event(enable_timing=True)
             self.ev_end = torch.cuda.Event(enable_timing=True)
 
+    def plan(self) -> dict:
+        """How the engine runs this group's epoch (nerfhip_group_plan): the row
+        variant ('regular' / 'ksplit'), the gradient row slices, the grids and
+        the launches per epoch."""
+        p = _native.NerfhipPlan()
+        _native.check(_native.load().nerfhip_group_plan(ctypes.byref(self.desc), ctypes.byref(p)))
+        return {"rows_variant": _native.ROWS_VARIANTS[p.rows_variant], "grad_split": p.grad_split,
+                "rows_workgroups": p.rows_workgroups, "params_workgroups": p.params_workgroups,
+                "launches_per_epoch": p.launches_per_epoch}
+
     def outputs(self, specs, group_seconds):
         N, D, n = self.N, self.D, self.n
         numel = float(N * D)
@@ -256,6 +267,7 @@ class _Group:
             p_cos_mean = p_cos.mean(-1)
         flops = [fit_flops(N, D, specs[i].config, E) for i in self.members]
         tot = sum(flops) or 1.0
+        plan = self.plan()
         outs = []
         for k, i in enumerate(self.members):
             P = specs[i].config.num_parameters(D)
@@ -271,7 +283,7 @@ class _Group:
                 row_mse=row_mse[k].copy(), final_mse=float(final_mse[k]), probes=probes,
                 train_time_seconds=group_seconds,
                 flop_share_seconds=group_seconds * flops[k] / tot,
-                group_seconds=group_seconds, device=self.device))
+                group_seconds=group_seconds, device=self.device, plan=dict(plan)))
         return outs
 
 

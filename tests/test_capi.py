@@ -89,3 +89,30 @@ def test_fit_rejects_before_touching_device(lib):
     assert lib.nerfhip_siren_forward(None, None) == -5
     g.W, g.precision = 256, 7
     assert lib.nerfhip_siren_fit(ctypes.byref(g), 1, streams) == -7      # unknown precision
+
+
+def _plan(lib, **kw):
+    g = _native.NerfhipGroup(**kw)
+    p = _native.NerfhipPlan()
+    rc = lib.nerfhip_group_plan(ctypes.byref(g), ctypes.byref(p))
+    return rc, p
+
+
+def test_group_plan(lib):
+    """nerfhip_group_plan (host only): BASELINE config 2, one medium fit at
+    seq 2048 in bf16x3 with the split-K workspace, takes the K-split row kernel
+    (one 16-row block per workgroup) and 16 gradient row slices; a 40-fit
+    sweep chunk the regular kernels, fused."""
+    rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=1,
+                  grad_partial=1)
+    assert rc == 0
+    assert (p.rows_variant, p.grad_split, p.rows_workgroups) == (1, 16, 2048 // 16)
+    assert p.params_workgroups == 16 * (2 * 4 + 1 * 2 + 256 // 64)      # 14 tiles x 16 slices
+    assert p.launches_per_epoch == 3
+    rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=40, L_max=3, epochs=2000, precision=1)
+    assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (0, 1, 2)
+    assert p.rows_workgroups == 8 * 32 * 5                            # XCD map: 40 fits x 32
+    rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=0)
+    assert rc == 0 and p.rows_variant == 0                            # fp32: regular rows
+    assert _plan(lib, W=100, D=128, N=64, n_fits=1, L_max=1, epochs=1)[0] == -1
+    assert lib.nerfhip_group_plan(None, None) == -5

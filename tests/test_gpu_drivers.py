@@ -102,6 +102,59 @@ def test_scan_points_vs_reference(gpu, golden_dir, seq_len):
         np.testing.assert_allclose(o.losses[::100][:5], r["losses_every100"][:5], rtol=1e-3)
 
 
+def test_config2_lone_medium_fit_vs_reference(gpu, golden_dir, sweep):
+    """BASELINE config 2 on its exact path: L0_H0_key_medium (seq 2048, 2000
+    epochs) alone, from its sweep-order init, against the reference's own
+    seed-0 sweep.  A lone fit takes the small-group kernels: K-split rows and
+    16 gradient row slices + k_adam_split (3 launches per epoch).  fit_siren,
+    the reference's entry point, drawing the same init from the same RNG
+    state, runs that same path (bitwise-equal result)."""
+    from nerf_attention import fit_siren
+    plan, specs = sweep
+    ref = _ref_sweep(golden_dir)
+    names = [p[0] for p in plan]
+    i = names.index("L0_H0_key_medium")
+    assert names[:i] == ["L0_H0_key_tiny", "L0_H0_key_small"]
+    out = engine.run_fits([specs[i]], 2000, devices=[0])[0]
+    assert out.plan["rows_variant"] == "ksplit", out.plan
+    assert out.plan["grad_split"] == 16 and out.plan["launches_per_epoch"] == 3, out.plan
+    cos = _cos(out)
+    assert abs(cos - ref["L0_H0_key_medium"]["final_cosine_mean"]) <= COS_TOL, cos
+    assert abs(out.final_mse / ref["L0_H0_key_medium"]["final_mse"] - 1) <= 0.05
+    cfg = plan[i][4]
+    torch.manual_seed(0)
+    for c in plan[0][4], plan[1][4]:                    # the sweep's first two inits
+        SIREN(c, 128)
+    res = fit_siren(specs[i].target, cfg, epochs=2000, device="cuda", verbose=False)
+    assert torch.equal(res.model.cpu().flat_parameters(), out.params.cpu())
+    assert res.final_cosine_mean == cos
+
+
+def test_config4_scan_all_layers_heads_vs_reference(gpu, golden_dir, tmp_path):
+    """BASELINE config 4 at its stated size for one length: medium on all 32
+    layers x 8 heads x K/V (512 fits) at seq 512, 200 epochs, through the
+    drop-in fit_kv_cache(select='all', configs=['medium']) from one
+    manual_seed(0).  The scaling experiment's fits (layers {0, 16, 31}, head 0;
+    experiments/scaling.py:160-168) match the reference trained from the same
+    sweep-order RNG state (scan_all_medium_e200.json, make_golden.py
+    scan_all); every fit's record is complete and finite."""
+    from nerf_attention.fit import fit_kv_cache
+    from nerf_attention.synthetic import write_kv_cache
+    g = json.loads((golden_dir / "scan_all_medium_e200.json").read_text())
+    kv = tmp_path / "kv"
+    write_kv_cache(kv, seq_len=g["seq_len"])
+    torch.manual_seed(g["seed"])
+    recs = fit_kv_cache(kv, tmp_path / "out", epochs=g["epochs"], device="cuda", select="all",
+                        configs=["medium"])
+    assert len(recs) == g["n_fits"] == 512
+    assert all(np.isfinite(r["final_cosine_mean"]) and np.isfinite(r["final_mse"]) for r in recs)
+    for r in g["records"]:
+        got = recs[r["index"]]
+        assert got["name"] == r["name"]
+        assert abs(got["final_cosine_mean"] - r["final_cosine_mean"]) <= COS_TOL, (r["name"], got)
+        assert abs(got["final_mse"] / r["final_mse"] - 1) <= 0.02, (r["name"], got)
+
+
 def _quick_cache(tmp):
     from nerf_attention.synthetic import extract_kv_cache_synthetic
     kv = Path(tmp) / "kv"

@@ -1,7 +1,8 @@
 """K-split row kernel co-residency probe (round 3).
 
-Runs the lone-fit K-split path (NERFHIP_ROWS_KS=1) with the LDS padding given
-by NERFHIP_KS_DYN_LDS (0 = two workgroups may share a CU) at seq 8192/16384 for
+Runs the lone-fit K-split path (NERFHIP_ROWS_KS=1), pad "0" = two workgroups
+may share a CU (NERFHIP_KS_SHARE_CU=1; the round-3 sessions varied the pad
+size through NERFHIP_KS_DYN_LDS, since replaced), at seq 8192/16384 for
 E = 0 and E = 3 epochs, then compares the final-eval ŷ with the torch forward
 of the final parameters, and characterises every wrong element: 16-row block,
 output tile J, feature-in-tile (= finalising wave w for fe = 4g + w), size.
@@ -29,9 +30,9 @@ if os.environ.get("KS_CASES"):      # e.g. "256,2,16384,0;256,2,8192,3"
 pads = os.environ.get("KS_PADS", "0,default").split(",")
 for pad in pads:
     if pad == "default":
-        os.environ.pop("NERFHIP_KS_DYN_LDS", None)
+        os.environ.pop("NERFHIP_KS_SHARE_CU", None)
     else:
-        os.environ["NERFHIP_KS_DYN_LDS"] = pad
+        os.environ["NERFHIP_KS_SHARE_CU"] = "1"
     for (W, L, N, E) in cases:
         cfg = SIRENConfig(W, L, 30.0, "x")
         keys, _ = kv_slice(0, 0, seq_len=N, num_layers=1, num_kv_heads=1)
