@@ -91,6 +91,9 @@ struct KArgs {
   uint16_t* wsplit;
   // row-step variant: 1 = the K-split kernel for small groups (k_step_rows_ks)
   int32_t rows_ks;
+  // diagnostic builds only (NERFHIP_STAMPS): per-wave s_memrealtime stamps of
+  // the parameter kernel, [blocks][4 waves][8] (NERFHIP_PSTAMPS = device address)
+  unsigned long long* pstamps;
 };
 template <int W, int D, bool X3> int launch_rows(const KArgs& a, hipStream_t st);
 template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t st);
@@ -120,7 +123,16 @@ __device__ unsigned long long* g_stamps = nullptr;
       g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] += (v); \
   } while (0)
 #define MEMTIME() __builtin_amdgcn_s_memtime()
+#define PSTAMP(k)                                                                      \
+  do {                                                                                 \
+    if (a.pstamps && (threadIdx.x & 63) == 0)                                          \
+      a.pstamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =             \
+          __builtin_amdgcn_s_memrealtime();                                            \
+  } while (0)
 #else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -1650,11 +1662,6 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
         lo[x][y][q] = 0.f;
       }
 
-  f4 st0[NPT], st1[NPT];
-  gload(st0, 0);
-  lstore(st0, lds, true);
-  gload(st1, 1);
-  __syncthreads();
   const uint16_t* a_base = lds + (wj * (TJ / 2) + lr) * kFx + 8 * h;
   const uint16_t* b_base = lds + (TJ + wk * (TK / WK) + lr) * kFx + 8 * h;
   auto rd = [&](const uint16_t* q) {
@@ -1665,9 +1672,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     return r;
   };
 
-  auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
-    // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
-    gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
+  auto mfma_block = [&](int rb) {
     const int off = (rb & 1) * BUFX;
     S8 av[NA], bv[NB];
 #pragma unroll
@@ -1681,6 +1686,24 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     // (measured slower, each 7-14 %: one accumulator per sub-tile; product-major
     // issue order across sub-tiles; operands loaded straight to registers
     // without LDS; a conflict-free LDS layout — this order and staging stay)
+  };
+  // stream the blocks: two in flight in registers, one in each LDS buffer.
+  // (Issuing every block's loads up front for split-K slices of 8 blocks —
+  // config 2's 224-workgroup grid — was bitwise equal and no faster: 20.7 vs
+  // 19.4 µs; its diagnostic stamps put the time in the prologue's dependent
+  // scalar loads, ≈3.3 µs, and the partial-slab stores, ≈6.5 µs, not in the
+  // block loads, profiles/r03/params_split_stamps.log)
+  f4 st0[NPT], st1[NPT];
+  gload(st0, 0);
+  PSTAMP(1);
+  lstore(st0, lds, true);
+  gload(st1, 1);
+  __syncthreads();
+  PSTAMP(2);
+  auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
+    // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
+    gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
+    mfma_block(rb);
     lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
     __syncthreads();
   };
@@ -1688,6 +1711,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     block(rb, st0, st1);
     block(rb + 1, st1, st0);
   }
+  PSTAMP(3);
 
   // Adam on the wave's (TJ/2)×(TK/WK) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
 #pragma unroll
@@ -1748,6 +1772,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
       }
     }
   }
+  PSTAMP(4);
 }
 
 // Tiles: dW[j0:j0+T][k0:k0+TK] on 4 waves, two workgroups per CU.  (WIDE:
@@ -1774,6 +1799,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, 
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   int fit, t;
   const int nt = C::tiles(a.L_max);
+  PSTAMP(0);
   if (!map_block(blockIdx.x, a.n_fits, nt * a.n_split, fit, t)) return;
   const int split = t / nt;
   t -= split * nt;
@@ -1863,6 +1889,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, 
 // copy.  One thread per canonical parameter index; grid (ceil(P/256), n_fits).
 // (W, D compile-time: the index splits and split-copy addresses fold to
 // shifts and multiplies)
+constexpr int kMaxSplitK = 16;   // most row slices of a split-K reduction (nerfhip_sizes.grad_split)
 template <int W, int D>
 __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   const int fit = blockIdx.y;
@@ -1870,8 +1897,21 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n_params(W, D, L)) return;
   const float* g = a.gpart + fit * a.gp_stride + i;
-  float gs = g[0];
-  for (int sp = 1; sp < a.n_split; ++sp) gs += g[sp * a.p_stride];
+  // every slice's load in flight at once (n_split <= kMaxSplitK, uniform):
+  // a runtime-count loop compiled to load → vmcnt(0) → add per slice, 15
+  // serial L2/HBM round trips (10.5 µs of config 2's 93 µs epoch)
+  // (unconditional loads of clamped slices: predicated ones became branches
+  // with a vmcnt(0) drain at every join)
+  float gv[kMaxSplitK];
+  const int ns = a.n_split;
+#pragma unroll
+  for (int sp = 0; sp < kMaxSplitK; ++sp) gv[sp] = g[(sp < ns ? sp : ns - 1) * a.p_stride];
+  float gs = gv[0];
+#pragma unroll
+  for (int sp = 1; sp < kMaxSplitK; ++sp) {
+    const float t = gs + gv[sp];
+    gs = sp < ns ? t : gs;             // slice order: the same sum as before
+  }
   float* P = a.params + fit * a.p_stride;
   float* M = a.m + fit * a.p_stride;
   float* V = a.v + fit * a.p_stride;
@@ -2027,7 +2067,7 @@ int validate(int W, int D, int N, int L_max, int epochs) {
   return NERFHIP_OK;
 }
 
-constexpr int64_t kMaxSplit = 16;
+constexpr int64_t kMaxSplit = kMaxSplitK;
 void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   const int64_t n_pad = ((int64_t)N + kRowPad - 1) / kRowPad * kRowPad;
   s->n_pad = n_pad;
@@ -2113,6 +2153,10 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   a.ws_stride = s.wsplit;
   a.wsplit = static_cast<uint16_t*>(g->wsplit);
   a.rows_ks = rows_ks_for(g, s) ? 1 : 0;
+#ifdef NERFHIP_STAMPS
+  if (const char* e = getenv("NERFHIP_PSTAMPS"))
+    a.pstamps = reinterpret_cast<unsigned long long*>(strtoull(e, nullptr, 0));
+#endif
   return a;
 }
 

@@ -27,7 +27,12 @@ def main():
              ("large8", SIRENConfig(512, 2, 30.0, "large"), 8, 256, 128),
              ("tiny12", SIRENConfig(64, 1, 30.0, "tiny"), 12, 192, 128),
              ("small3", SIRENConfig(128, 1, 30.0, "small"), 3, 320, 64),
-             ("w256d64", SIRENConfig(256, 2, 60.0, "x"), 10, 256, 64)]
+             ("w256d64", SIRENConfig(256, 2, 60.0, "x"), 10, 256, 64),
+             # split-K slices of exactly 8 blocks (the prefetch-all parameter path)
+             ("medium1_2048", SIRENConfig(256, 2, 30.0, "medium"), 1, 2048, 128),
+             ("medium2_1024", SIRENConfig(256, 2, 30.0, "medium"), 2, 1024, 128),
+             ("small5_2048", SIRENConfig(128, 1, 30.0, "small"), 5, 2048, 128),
+             ("tiny5_2048", SIRENConfig(64, 1, 30.0, "tiny"), 5, 2048, 128)]
     for name, cfg, n, N, D in cases:
         specs = []
         for i in range(n):
