@@ -99,14 +99,50 @@ def host_cpus() -> dict:
             "threads": min(logical, quota) if quota else logical}
 
 
+def _pin_threads(n: int):
+    """While the CPU baseline runs, keep every thread of this process on n
+    fixed CPUs of its affinity mask when the mask is wider than its cgroup
+    quota (the GPU box: 256 CPUs in the mask, a 16-CPU quota).  Unpinned, the
+    16 torch threads wander over 256 CPUs of a shared two-socket host, and the
+    repeat spread of the samples was 37-69 % (BENCH_r02, round 3).  Returns
+    (saved masks, the CPUs) or None."""
+    mask = sorted(os.sched_getaffinity(0))
+    if len(mask) <= n:
+        return None
+    cpus = set(mask[:n])
+    saved = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            saved[int(tid)] = os.sched_getaffinity(int(tid))
+            os.sched_setaffinity(int(tid), cpus)
+        except OSError:
+            pass
+    return saved, cpus
+
+
+def _unpin_threads(pinned) -> None:
+    if not pinned:
+        return
+    for tid, m in pinned[0].items():
+        try:
+            os.sched_setaffinity(tid, m)
+        except OSError:
+            pass
+
+
 def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
-                 warmup_epochs: int = 10) -> dict:
+                 warmup_epochs: int = 10, sample_s: float | None = 0.6) -> dict:
     """Time the package's own host path (host_fit.fit_on_host: the reference
     loop, siren.py:80-149, in eager PyTorch) on every architecture: one untimed
     warm-up fit of `warmup_epochs` per architecture (thread pool, allocator,
-    first-touch), then `repeats` fits of `sample_epochs` epochs, on every CPU
-    this process may use.  The median per-epoch time of each architecture is
-    extrapolated to the 280-fit sweep (dense cost is data-independent)."""
+    first-touch; it also prices the architecture), then `repeats` rounds over
+    the architectures, on every CPU this process may use.  Each timed fit runs
+    about `sample_s` seconds (its epoch count from the warm-up's per-epoch time,
+    at least `sample_epochs` — so the cheap architectures are not timed over
+    0.1-s windows that a co-tenant's burst or a CFS quota period dominates);
+    sample_s=None: exactly `sample_epochs` each.  The median per-epoch time of
+    each architecture is extrapolated to the 280-fit sweep (dense cost is
+    data-independent)."""
     from nerf_attention import CONFIGS_FULL, SIREN
     from nerf_attention.host_fit import fit_on_host
     from nerf_attention.synthetic import kv_slice
@@ -114,8 +150,11 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
     threads = cpus["threads"]
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
+    pinned = _pin_threads(threads)   # see _pin_threads: restored below
+    cpus["pinned_cpus"] = pinned and len(pinned[1])
     keys, _ = kv_slice(16, 2, seq_len=seq_len)
     samples = {c.name: [] for c in CONFIGS_FULL}
+    epochs_of = {}
 
     def one(cfg, epochs):
         torch.manual_seed(0)
@@ -124,28 +163,35 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
 
     try:
         for cfg in CONFIGS_FULL:
-            one(cfg, warmup_epochs)
+            t = one(cfg, warmup_epochs)
+            epochs_of[cfg.name] = sample_epochs if sample_s is None else \
+                max(sample_epochs, int(round(sample_s / max(t, 1e-6))))
         for _ in range(repeats):
             for cfg in CONFIGS_FULL:
-                samples[cfg.name].append(one(cfg, sample_epochs))
+                samples[cfg.name].append(one(cfg, epochs_of[cfg.name]))
     finally:
         torch.set_num_threads(prev)
+        _unpin_threads(pinned)
     per_epoch = {k: float(np.median(v)) for k, v in samples.items()}
     sweep_s = 40 * 2000 * sum(per_epoch.values())
     # spread of the repeats around the median, worst architecture
     spread = max((max(v) - min(v)) / float(np.median(v)) for v in samples.values())
+    timed_s = sum(epochs_of[k] * sum(v) for k, v in samples.items())
     return {"value": 280.0 / sweep_s, "unit": "fits/s", "cores": threads, "kind": "port",
             "port": "package host path (nerf_attention/host_fit.py)",
             "sample": f"nerf_attention/host_fit.py (the reference loop in eager PyTorch), each of "
                       f"the 7 archs: 1 untimed warm-up of {warmup_epochs} epochs, then "
-                      f"{repeats} repeats x {sample_epochs} epochs on synthetic L16 H2 key "
-                      f"[{seq_len},128]; median per-epoch time per arch; sweep = "
+                      f"{repeats} rounds of one fit per arch of ~{sample_s}s (epochs "
+                      f"{epochs_of}) on synthetic L16 H2 key [{seq_len},128], {timed_s:.1f}s "
+                      f"timed in all; median per-epoch time per arch; sweep = "
                       f"40x2000x(sum of medians) = {sweep_s:.0f}s; {cpus['model']}, "
                       f"{threads} torch threads (affinity {cpus['affinity_cpus']} CPUs, "
                       f"cgroup quota {cpus['cgroup_cpu_quota']})",
             "host": cpus, "repeat_spread": round(spread, 4),
             "repeat_spread_kind": "(max - min) / median of the timed repeats, worst arch",
-            "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()}}
+            "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()},
+            "spread_per_arch": {k: round((max(v) - min(v)) / float(np.median(v)), 4)
+                                for k, v in samples.items()}}
 
 
 def e2e_fit_kv_cache(seq_len: int, epochs: int, precision: str) -> dict:
