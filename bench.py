@@ -63,6 +63,15 @@ GOLDEN_SWEEP = ROOT / "tests" / "golden" / "sweep_ref_seed0_e2000.json"
 PMC_TRAFFIC = ROOT / "profiles" / "pmc_traffic.json"
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One progress line on stderr (the JSON result stays the only stdout line):
+    a long default run under a profiler keeps writing, and a hang shows where."""
+    print(f"[bench {time.perf_counter() - _T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def rows_flops(N, D, cfgs):
     """k_step_rows: forward + backward-dX GEMMs of one epoch (2·N·K·M each)."""
     return sum(4.0 * N * (c.hidden_layers * c.hidden_features ** 2 + c.hidden_features * D)
@@ -166,9 +175,10 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
             t = one(cfg, warmup_epochs)
             epochs_of[cfg.name] = sample_epochs if sample_s is None else \
                 max(sample_epochs, int(round(sample_s / max(t, 1e-6))))
-        for _ in range(repeats):
+        for rep in range(repeats):
             for cfg in CONFIGS_FULL:
                 samples[cfg.name].append(one(cfg, epochs_of[cfg.name]))
+            progress(f"cpu baseline round {rep + 1}/{repeats}")
     finally:
         torch.set_num_threads(prev)
         _unpin_threads(pinned)
@@ -338,10 +348,12 @@ def main() -> None:
     mine = farm.rank_share(costs, world, rank, widths)
     job = engine.FitJob([specs[i] for i in mine], args.epochs, devices=[local],
                         precision=args.precision)
+    progress(f"rank {rank}: {len(mine)} fits in {len(job.groups)} groups, warm-up")
 
     for _ in range(args.warmup):
         job.launch()
         job.wait()
+    progress("warm-up done, timed steps")
 
     barrier = farm.barrier
     barrier()
@@ -354,6 +366,7 @@ def main() -> None:
             acc[0] += t.rows_ms
             acc[1] += t.params_ms
             acc[2] += t.launches
+        progress("timed step done")
     barrier()
     elapsed = time.perf_counter() - t0
     t_max = farm.max_over_ranks(elapsed)
@@ -403,6 +416,7 @@ def main() -> None:
                 hbm = traffic["bytes"] / (avg_ms * 1e-3) / 1e9
             gcf = [specs[mine[i]].config for i in g.members]
             g_flops = (rows_flops if "rows" in kname else params_flops)(N, 128, gcf)
+            progress(f"isolated {kname}")
             iso = isolated_kernel([specs[mine[i]] for i in g.members], kname, g_flops,
                                   args.precision, peak, local)
             iso["fits"] = g.n
@@ -478,12 +492,15 @@ def main() -> None:
         }
         also = args.also_fp32 if args.also_fp32 is not None else args.precision != "fp32"
         if world == 1 and also:
+            progress("fp32 sweep")
             line["fp32_mfma"] = fp32_sweep([specs[i] for i in mine], args.epochs, local, plan,
                                            all_cos if parity else None, n_total)
         if world == 1 and not args.no_e2e:
+            progress("e2e fit_kv_cache")
             line["e2e_fit_kv_cache"] = e2e_fit_kv_cache(args.seq_len, args.epochs, args.precision)
             line["e2e_fits_per_s"] = line["e2e_fit_kv_cache"]["fits_per_s"]
         if world == 1 and not args.no_cpu_baseline:
+            progress("cpu baseline")
             line["cpu_baseline"] = cpu_baseline(args.seq_len, args.cpu_sample_epochs)
         print(json.dumps(line), flush=True)
     if world > 1:
