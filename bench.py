@@ -108,37 +108,6 @@ def host_cpus() -> dict:
             "threads": min(logical, quota) if quota else logical}
 
 
-def _pin_threads(n: int):
-    """While the CPU baseline runs, keep every thread of this process on n
-    fixed CPUs of its affinity mask when the mask is wider than its cgroup
-    quota (the GPU box: 256 CPUs in the mask, a 16-CPU quota).  Unpinned, the
-    16 torch threads wander over 256 CPUs of a shared two-socket host, and the
-    repeat spread of the samples was 37-69 % (BENCH_r02, round 3).  Returns
-    (saved masks, the CPUs) or None."""
-    mask = sorted(os.sched_getaffinity(0))
-    if len(mask) <= n:
-        return None
-    cpus = set(mask[:n])
-    saved = {}
-    for tid in os.listdir("/proc/self/task"):
-        try:
-            saved[int(tid)] = os.sched_getaffinity(int(tid))
-            os.sched_setaffinity(int(tid), cpus)
-        except OSError:
-            pass
-    return saved, cpus
-
-
-def _unpin_threads(pinned) -> None:
-    if not pinned:
-        return
-    for tid, m in pinned[0].items():
-        try:
-            os.sched_setaffinity(tid, m)
-        except OSError:
-            pass
-
-
 def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
                  warmup_epochs: int = 10, sample_s: float | None = 0.6) -> dict:
     """Time the package's own host path (host_fit.fit_on_host: the reference
@@ -159,8 +128,6 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
     threads = cpus["threads"]
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
-    pinned = _pin_threads(threads)   # see _pin_threads: restored below
-    cpus["pinned_cpus"] = pinned and len(pinned[1])
     keys, _ = kv_slice(16, 2, seq_len=seq_len)
     samples = {c.name: [] for c in CONFIGS_FULL}
     epochs_of = {}
@@ -181,7 +148,6 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
             progress(f"cpu baseline round {rep + 1}/{repeats}")
     finally:
         torch.set_num_threads(prev)
-        _unpin_threads(pinned)
     per_epoch = {k: float(np.median(v)) for k, v in samples.items()}
     sweep_s = 40 * 2000 * sum(per_epoch.values())
     # spread of the repeats around the median, worst architecture
