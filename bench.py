@@ -104,8 +104,26 @@ def host_cpus() -> dict:
                 break
     except OSError:
         pass
+    # Under a CPU quota, leave headroom for the process's other threads (the
+    # Python main thread, the HIP runtime's, a profiler's): torch threads that
+    # use the whole quota get the cgroup throttled every CFS period, which made
+    # the baseline's repeats spread by 37-67 % on the GPU box (round 3)
+    threads = min(logical, max(1, quota - 4) if quota and quota > 8 else quota) if quota \
+        else logical
     return {"affinity_cpus": logical, "cgroup_cpu_quota": quota, "model": model,
-            "threads": min(logical, quota) if quota else logical}
+            "threads": threads}
+
+
+def cgroup_throttled_us() -> int | None:
+    """Microseconds this cgroup has been throttled by its CPU quota (cpu.stat)."""
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k == "throttled_usec":
+                return int(v)
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
@@ -130,6 +148,7 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
     torch.set_num_threads(threads)
     keys, _ = kv_slice(16, 2, seq_len=seq_len)
     samples = {c.name: [] for c in CONFIGS_FULL}
+    thr0 = cgroup_throttled_us()
     epochs_of = {}
 
     def one(cfg, epochs):
@@ -153,6 +172,9 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
     # spread of the repeats around the median, worst architecture
     spread = max((max(v) - min(v)) / float(np.median(v)) for v in samples.values())
     timed_s = sum(epochs_of[k] * sum(v) for k, v in samples.items())
+    thr1 = cgroup_throttled_us()
+    cpus["throttled_s_during_baseline"] = (thr1 - thr0) / 1e6 if thr0 is not None and thr1 is not None \
+        else None
     return {"value": 280.0 / sweep_s, "unit": "fits/s", "cores": threads, "kind": "port",
             "port": "package host path (nerf_attention/host_fit.py)",
             "sample": f"nerf_attention/host_fit.py (the reference loop in eager PyTorch), each of "
@@ -162,7 +184,8 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
                       f"timed in all; median per-epoch time per arch; sweep = "
                       f"40x2000x(sum of medians) = {sweep_s:.0f}s; {cpus['model']}, "
                       f"{threads} torch threads (affinity {cpus['affinity_cpus']} CPUs, "
-                      f"cgroup quota {cpus['cgroup_cpu_quota']})",
+                      f"cgroup quota {cpus['cgroup_cpu_quota']}, 4 left for the process's "
+                      f"other threads)",
             "host": cpus, "repeat_spread": round(spread, 4),
             "repeat_spread_kind": "(max - min) / median of the timed repeats, worst arch",
             "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()},
