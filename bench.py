@@ -104,12 +104,7 @@ def host_cpus() -> dict:
                 break
     except OSError:
         pass
-    # Under a CPU quota, leave headroom for the process's other threads (the
-    # Python main thread, the HIP runtime's, a profiler's): torch threads that
-    # use the whole quota get the cgroup throttled every CFS period, which made
-    # the baseline's repeats spread by 37-67 % on the GPU box (round 3)
-    threads = min(logical, max(1, quota - 4) if quota and quota > 8 else quota) if quota \
-        else logical
+    threads = min(logical, quota) if quota else logical
     return {"affinity_cpus": logical, "cgroup_cpu_quota": quota, "model": model,
             "threads": threads}
 
@@ -184,8 +179,7 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
                       f"timed in all; median per-epoch time per arch; sweep = "
                       f"40x2000x(sum of medians) = {sweep_s:.0f}s; {cpus['model']}, "
                       f"{threads} torch threads (affinity {cpus['affinity_cpus']} CPUs, "
-                      f"cgroup quota {cpus['cgroup_cpu_quota']}, 4 left for the process's "
-                      f"other threads)",
+                      f"cgroup quota {cpus['cgroup_cpu_quota']})",
             "host": cpus, "repeat_spread": round(spread, 4),
             "repeat_spread_kind": "(max - min) / median of the timed repeats, worst arch",
             "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()},
