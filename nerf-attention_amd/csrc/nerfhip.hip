@@ -102,7 +102,10 @@ template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t s
 namespace {
 using nerfhip_detail::KArgs;
 
-constexpr int kRowPad = 64;    // n_pad granule: a whole number of row workgroups
+#ifndef NERFHIP_ROWPAD
+#define NERFHIP_ROWPAD 64
+#endif
+constexpr int kRowPad = NERFHIP_ROWPAD;   // n_pad granule: a whole number of row workgroups
 
 
 
@@ -758,7 +761,13 @@ template <int W> struct RowsCfg {
   // (W = 256 at one wave per SIMD — no VGPR spills, 512 registers — measured
   // 25 % slower: the second wave's MFMAs are what fill the epilogue gaps)
   static constexpr int WAVES_PER_SIMD = W >= 512 ? 1 : 2;
-  static constexpr int NWAVES = 4;
+// experiment knob: waves (16 rows each) per W = 256 workgroup.  8 (with
+// NERFHIP_ROWPAD=128): isolated 40-fit launch 8 % slower, 200-epoch sweep
+// +1.2 %, results equal only to rounding (profiles/r03/rows_w256_8waves.log)
+#ifndef NERFHIP_ROWS_NWAVES_256
+#define NERFHIP_ROWS_NWAVES_256 4
+#endif
+  static constexpr int NWAVES = W == 256 ? NERFHIP_ROWS_NWAVES_256 : 4;
   static constexpr int THREADS = 64 * NWAVES, ROWS = 16 * NWAVES;
 };
 
