@@ -55,11 +55,14 @@ class FitOutput:
     row_mse: np.ndarray           # [seq_len] final per-row MSE (siren.py:125)
     final_mse: float              # siren.py:123
     probes: list = field(default_factory=list)  # (epoch, norm_mse, real_mse, cos)
-    # the reference's quantity (siren.py:96,117): wall clock of the epoch loop
-    # that trained this fit — here its group's loop, shared by every fit of the
-    # group (they train concurrently, so the sum over fits overcounts)
+    # the reference's quantity (siren.py:96,117) is the wall clock of the epoch
+    # loop that trained this fit, and its sum over a sequential sweep is the
+    # sweep's training time.  Fits that train concurrently have no loop of their
+    # own, so each gets the job's wall clock x its share of the job's FLOPs
+    # (SURVEY §8d model): a lone fit (fit_siren) gets its own loop time, and the
+    # sum over a job's fits is the job's wall clock, as in the reference
     train_time_seconds: float = 0.0
-    flop_share_seconds: float = 0.0   # group time x this fit's share of its FLOPs
+    flop_share_seconds: float = 0.0   # group time x this fit's share of its group's FLOPs
     group_seconds: float = 0.0
     device: int = 0
     plan: dict = field(default_factory=dict)   # how its group ran (_Group.plan)
@@ -246,7 +249,7 @@ class _Group:
                 "rows_workgroups": p.rows_workgroups, "params_workgroups": p.params_workgroups,
                 "launches_per_epoch": p.launches_per_epoch}
 
-    def outputs(self, specs, group_seconds):
+    def outputs(self, specs, group_seconds, job_seconds=None, job_flops=None):
         N, D, n = self.N, self.D, self.n
         numel = float(N * D)
         E = self.epochs
@@ -281,7 +284,8 @@ class _Group:
                 target_std=std[k].view(1, D).clone(),
                 losses=[float(x) for x in losses[k]], row_cos=row_cos[k].copy(),
                 row_mse=row_mse[k].copy(), final_mse=float(final_mse[k]), probes=probes,
-                train_time_seconds=group_seconds,
+                train_time_seconds=(job_seconds * flops[k] / job_flops
+                                    if job_seconds is not None and job_flops else group_seconds),
                 flop_share_seconds=group_seconds * flops[k] / tot,
                 group_seconds=group_seconds, device=self.device, plan=dict(plan)))
         return outs
@@ -394,8 +398,12 @@ class FitJob:
 
     def outputs(self) -> list:
         outs = [None] * len(self.specs)
-        for g, secs in zip(self.groups, self.group_seconds()):
-            for i, o in zip(g.members, g.outputs(self.specs, secs)):
+        secs = self.group_seconds()
+        job_s = max(secs) if secs else 0.0          # the groups start together
+        job_f = sum(fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config,
+                              self.epochs) for s in self.specs)
+        for g, gs in zip(self.groups, secs):
+            for i, o in zip(g.members, g.outputs(self.specs, gs, job_s, job_f)):
                 outs[i] = o
         return outs
 

@@ -13,10 +13,11 @@ and then ALL fits are trained together on the HIP engine (grouped by width,
 one stream per group, optionally over several GPUs).  The per-fit progress
 lines are printed afterwards, in the reference order.
 
-`train_time_seconds` keeps the reference's meaning (siren.py:96,117): the
-wall clock of the epoch loop that trained the fit.  Fits of a group train
-concurrently in one loop, so they share that figure and its sum over fits
-overcounts the sweep (the sweep's wall clock is printed at the end).
+`train_time_seconds` (siren.py:96,117: the wall clock of the fit's epoch
+loop; summed over the reference's sequential sweep, its training time): the
+fits here train concurrently, so each gets the job's wall clock times its
+share of the job's FLOPs — a lone fit its own loop time, and the sum over a
+sweep the sweep's training wall clock (per GPU), as in the reference.
 
 With `gpus=N` (or `--gpus N`) the fits are farmed over N GPUs, one worker
 process per GPU (farm.run_farm), the same one-process-per-GPU design as

@@ -60,6 +60,10 @@ def test_sweep_280_vs_reference(gpu, golden_dir, sweep):
     assert d.size == 280 and d.max() <= COS_TOL, (d.max(), plan[int(d.argmax())][0])
     mse = np.array([o.final_mse / ref[p[0]]["final_mse"] for p, o in zip(plan, outs)])
     assert np.abs(mse - 1).max() <= 0.05
+    # train_time_seconds: the job's wall clock split by FLOP share, so the sweep's
+    # records sum to its training wall clock, as the reference's sequential ones do
+    wall = max(o.group_seconds for o in outs)
+    assert abs(sum(o.train_time_seconds for o in outs) / wall - 1) <= 1e-6
 
 
 @pytest.mark.parametrize("world,rank", [(8, 0), (2, 1)])
