@@ -91,6 +91,8 @@ struct KArgs {
   uint16_t* wsplit;
   // row-step variant: 1 = the K-split kernel for small groups (k_step_rows_ks)
   int32_t rows_ks;
+  // split-K parameter step on 64 × 64 tiles (ParamsCfg SMALL; split_for)
+  int32_t small_tiles;
   // diagnostic builds only (NERFHIP_STAMPS): per-wave s_memrealtime stamps of
   // the parameter kernel, [blocks][4 waves][8] (NERFHIP_PSTAMPS = device address)
   unsigned long long* pstamps;
@@ -1788,9 +1790,13 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
 // T × 256 tiles on 8 waves, one workgroup per CU, reads each dZ column block
 // once instead of W/128 times — a quarter less operand traffic — yet measured
 // 7 % slower at W = 256 and 512.)
-template <int W, int D, bool X3> struct ParamsCfg {
+// SMALL: 64 × 64 tiles for the split-K launches of small bf16x3 groups with
+// W >= 256 (split_for decides): 3.1x the tiles of 128 × 128, so the same grid
+// needs fewer row slices — fewer partial-slab bytes written and read back by
+// k_adam_split, the split step's floor.
+template <int W, int D, bool X3, bool SMALL = false> struct ParamsCfg {
   static constexpr bool WIDE = false;
-  static constexpr int T = W < 128 ? W : 128;          // hidden-layer tile rows (j)
+  static constexpr int T = SMALL ? 64 : (W < 128 ? W : 128);   // hidden-layer tile rows (j)
   static constexpr int TK = WIDE ? 256 : T;            // tile columns (k), hidden and final
   static constexpr int NW = WIDE ? 8 : 4, THREADS = 64 * NW;
   static constexpr int MINB = WIDE ? 1 : 2;            // workgroups per CU (launch bound)
@@ -1800,10 +1806,11 @@ template <int W, int D, bool X3> struct ParamsCfg {
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
-template <int W, int D, bool X3>
-__global__ void __launch_bounds__((ParamsCfg<W, D, X3>::THREADS), (ParamsCfg<W, D, X3>::MINB))
+template <int W, int D, bool X3, bool SMALL = false>
+__global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
+                                  (ParamsCfg<W, D, X3, SMALL>::MINB))
     k_step_params(KArgs a) {
-  using C = ParamsCfg<W, D, X3>;
+  using C = ParamsCfg<W, D, X3, SMALL>;
   constexpr int LDS_F = X3 ? 2 * 3 * (C::T + C::TK) * kFx / 2 : 2 * (2 * C::T) * kFs;
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
   int fit, t;
@@ -2098,26 +2105,49 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   s->wsplit = xs_size(W, D, L_max);
 }
 
-// Row slices of a small group's split-K gradient reduction: the most the
-// workspace allows (grad_split, <= 16) while the split grid, fits × weight
-// tiles × slices, stays within kSplitGrid workgroups (two per CU), or
-// NERFHIP_GRAD_SPLIT_MAX.  Measured (profiles/r02/ab_rows_ks.log "split 16"):
-// one medium fit (14 tiles) 8 → 16 slices −9 % parameter-kernel time; one
-// wide fit at 8192 (60 tiles) 16 slices +9 % (the grid passes 512 there).
+// Split-K grid limit (see split_for).  Measured with 128 × 128 tiles
+// (profiles/r02/ab_rows_ks.log "split 16"): one medium fit (14 tiles) 8 → 16
+// slices −9 % parameter-kernel time; one wide fit at 8192 (60 tiles) 16
+// slices +9 % (the grid passes 512 there).
 constexpr int64_t kSplitGrid = 512;
-int64_t param_tiles(int W, int D, int L) {   // ParamsCfg<W, D, X3>::tiles(L)
-  const int T = W < 128 ? W : 128, nt = W / T, TD = D < T ? D : T;
+int64_t param_tiles(int W, int D, int L, bool small = false) {   // ParamsCfg<W, D, X3, small>::tiles(L)
+  const int T = small ? 64 : (W < 128 ? W : 128), nt = W / T, TD = D < T ? D : T;
   return (int64_t)L * nt * nt + (int64_t)(D / TD) * nt + W / 64;
 }
-int32_t split_for(const nerfhip_group* g, const nerfhip_sizes& s) {
+// Row slices of a small group's split-K gradient reduction, and its tiles.
+// A bf16x3 group with W >= 256 takes 64 × 64 tiles (ParamsCfg SMALL) when
+// that grid still allows at least kSmallMinSplit slices: the split step's time
+// is mostly its fixed costs and the partial-slab bytes (slices × params), and
+// 3.1x the tiles reach the same grid with a quarter of the slices.  One
+// medium fit at 2048: 44 tiles × 8 slices, parameter step 19.7 → 13.7 µs,
+// config 2 0.0919 → 0.0846 ms per epoch; the wide fit at 8192 (216 small
+// tiles would allow 2 slices) keeps 128 × 128 × 8, which measured 3.5 %
+// faster than small tiles there (profiles/r03/split_small_tiles.log).
+// Otherwise: the most slices the workspace allows (grad_split, <= 16) while
+// fits × tiles × slices stays within kSplitGrid (two per CU).  Overrides:
+// NERFHIP_GRAD_SPLIT_MAX caps the slices; NERFHIP_SPLIT_T128=1 keeps
+// 128 × 128 tiles.
+constexpr int64_t kSmallMinSplit = 8;
+int32_t split_for(const nerfhip_group* g, const nerfhip_sizes& s, bool* small_tiles) {
   const char* e = getenv("NERFHIP_GRAD_SPLIT_MAX");
-  int64_t sp = s.grad_split;
-  if (e) {
-    while (sp > 1 && sp > atoi(e)) sp /= 2;
-  } else {
-    const int64_t grid = (int64_t)g->n_fits * param_tiles(g->W, g->D, g->L_max);
+  const char* t128 = getenv("NERFHIP_SPLIT_T128");
+  int64_t cap = s.grad_split;
+  if (e)
+    while (cap > 1 && cap > atoi(e)) cap /= 2;
+  *small_tiles = false;
+  if (g->precision == NERFHIP_PRECISION_BF16X3 && g->W >= 256 && !(t128 && t128[0] == '1')) {
+    const int64_t grid = (int64_t)g->n_fits * param_tiles(g->W, g->D, g->L_max, true);
+    int64_t sp = cap;
     while (sp > 2 && grid * sp > kSplitGrid) sp /= 2;
+    if (sp >= kSmallMinSplit) {
+      *small_tiles = true;
+      return (int32_t)sp;
+    }
   }
+  if (e) return (int32_t)cap;
+  int64_t sp = cap;
+  const int64_t grid = (int64_t)g->n_fits * param_tiles(g->W, g->D, g->L_max);
+  while (sp > 2 && grid * sp > kSplitGrid) sp /= 2;
   return (int32_t)sp;
 }
 
@@ -2155,7 +2185,9 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   // F.mse_loss backward: grad = (2/numel)·(ŷ−y), the 2/numel a python float
   // rounded to fp32 (TORCH/_decomp/decompositions.py:393-397).
   a.grad_scale = (float)(2.0 / ((double)g->N * (double)g->D));
-  a.n_split = (g->grad_partial && g->n_fits < kXcdMinFits) ? split_for(g, s) : 1;
+  bool small = false;
+  a.n_split = (g->grad_partial && g->n_fits < kXcdMinFits) ? split_for(g, s, &small) : 1;
+  a.small_tiles = small && a.n_split > 1;
   a.gp_stride = s.grad_partial;
   a.gpart = g->grad_partial;
   a.x3 = g->precision == NERFHIP_PRECISION_BF16X3;
@@ -2215,6 +2247,16 @@ int launch_rows(const KArgs& a, hipStream_t st) {
 
 template <int W, int D, bool X3>
 int launch_params(const KArgs& a, hipStream_t st) {
+  if constexpr (X3 && W >= 256) {
+    if (a.small_tiles) {
+      using CS = ParamsCfg<W, D, X3, true>;
+      const int grid_s = grid_for(a.n_fits, CS::tiles(a.L_max) * a.n_split);
+      hipLaunchKernelGGL((k_step_params<W, D, X3, true>), dim3(grid_s), dim3(CS::THREADS), 0, st, a);
+      const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
+      hipLaunchKernelGGL((k_adam_split<W, D>), dim3(blocks, a.n_fits), dim3(256), 0, st, a);
+      return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+    }
+  }
   const int grid = grid_for(a.n_fits, ParamsCfg<W, D, X3>::tiles(a.L_max) * a.n_split);
   hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS), 0,
                      st, a);
@@ -2563,7 +2605,8 @@ int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out) {
   out->rows_variant = a.rows_ks ? NERFHIP_ROWS_KSPLIT : NERFHIP_ROWS_REGULAR;
   out->grad_split = a.n_split;
   out->rows_workgroups = grid_for(a.n_fits, (int)(s.n_pad / rows_per_wg));
-  out->params_workgroups = grid_for(a.n_fits, (int)param_tiles(g->W, g->D, g->L_max) * a.n_split);
+  out->params_workgroups =
+      grid_for(a.n_fits, (int)param_tiles(g->W, g->D, g->L_max, a.small_tiles != 0) * a.n_split);
   out->launches_per_epoch = a.n_split > 1 ? 3 : 2;
   out->reserved = 0;
   return NERFHIP_OK;

@@ -110,7 +110,8 @@ def test_config2_lone_medium_fit_vs_reference(gpu, golden_dir, sweep):
     """BASELINE config 2 on its exact path: L0_H0_key_medium (seq 2048, 2000
     epochs) alone, from its sweep-order init, against the reference's own
     seed-0 sweep.  A lone fit takes the small-group kernels: K-split rows and
-    16 gradient row slices + k_adam_split (3 launches per epoch).  fit_siren,
+    8 gradient row slices on 64 x 64 tiles + k_adam_split (3 launches per
+    epoch).  fit_siren,
     the reference's entry point, drawing the same init from the same RNG
     state, runs that same path (bitwise-equal result)."""
     from nerf_attention import fit_siren
@@ -121,7 +122,8 @@ def test_config2_lone_medium_fit_vs_reference(gpu, golden_dir, sweep):
     assert names[:i] == ["L0_H0_key_tiny", "L0_H0_key_small"]
     out = engine.run_fits([specs[i]], 2000, devices=[0])[0]
     assert out.plan["rows_variant"] == "ksplit", out.plan
-    assert out.plan["grad_split"] == 16 and out.plan["launches_per_epoch"] == 3, out.plan
+    assert out.plan["grad_split"] == 8 and out.plan["launches_per_epoch"] == 3, out.plan
+    assert out.plan["params_workgroups"] == 8 * 44, out.plan      # 64 x 64 tiles
     cos = _cos(out)
     assert abs(cos - ref["L0_H0_key_medium"]["final_cosine_mean"]) <= COS_TOL, cos
     assert abs(out.final_mse / ref["L0_H0_key_medium"]["final_mse"] - 1) <= 0.05
