@@ -82,7 +82,7 @@ typedef struct nerfhip_group {
   int32_t D;               /* d_head = out_features                            */
   int32_t N;               /* seq_len                                         */
   int32_t n_fits;
-  int32_t L_max;           /* max hidden_layers over the group                 */
+  int32_t L_max;           /* max hidden_layers over the group (one fit: its own) */
   int32_t epochs;
   int32_t log_every;       /* probe period (siren.py:107); 0 = no probes       */
   int32_t device;          /* HIP device ordinal the buffers and stream live on */
@@ -114,7 +114,7 @@ typedef struct nerfhip_group {
                                  reduced in grad_split row slices (partial
                                  slabs, then a fixed-order sum + Adam): a small
                                  group otherwise fills only a few workgroups.
-                                 Deterministic; the split depends on N only.   */
+                                 Deterministic; slices and tiles depend on the group shape only. */
   void* wsplit;               /* [n] uint16 workspace, BF16X3 only (else NULL):
                                  every weight as exact bf16 split planes, in
                                  the forward and the transposed orientation,

@@ -371,6 +371,13 @@ __device__ __forceinline__ bool map_block(int b, int n_fits, int n_tiles, int& f
   return fit < n_fits;
 }
 
+// hidden_layers of a group's fit: a one-fit group's is L_max (nerfhip.h), a
+// kernel argument — no dependent load of fit_layers in front of the tile
+// decode of a lone fit's kernels (config 2's launches are latency-bound)
+__device__ __forceinline__ int fit_layers_of(const KArgs& a, int fit) {
+  return a.n_fits == 1 ? a.L_max : a.fit_layers[fit];
+}
+
 __host__ __device__ inline int64_t off_hidden_w(int W, int i) {  // i = 1..L
   return 2 * (int64_t)W + (int64_t)(i - 1) * ((int64_t)W * W + W);
 }
@@ -794,7 +801,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   const int lane = tid & 63, wave = tid >> 6;
   const int c = lane & 15, g = lane >> 4;
   float* stash = lds + WBUF + 2 * KMAX + wave * STASH + lane * 4;
-  const int L = a.fit_layers[fit];
+  const int L = fit_layers_of(a, fit);
   const float om = a.fit_omega[fit];
   const int n_pad = a.n_pad;
   const int rblk = tile * NWV + wave;         // 16-row block
@@ -1225,7 +1232,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, g = lane >> 4;
-  const int L = a.fit_layers[fit];
+  const int L = fit_layers_of(a, fit);
   const float om = a.fit_omega[fit];
   const int r = rblk * 16 + c;
   const bool valid = r < a.N;
@@ -1819,7 +1826,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
   if (!map_block(blockIdx.x, a.n_fits, nt * a.n_split, fit, t)) return;
   const int split = t / nt;
   t -= split * nt;
-  const int L = a.fit_layers[fit];
+  const int L = fit_layers_of(a, fit);
   if (t >= C::tiles(L)) return;
   const int nb = a.n_pad / 16 / a.n_split, rb0 = split * nb;
   float* G = a.n_split > 1 ? a.gpart + fit * a.gp_stride + split * a.p_stride : nullptr;
@@ -1906,28 +1913,22 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
 // (W, D compile-time: the index splits and split-copy addresses fold to
 // shifts and multiplies)
 constexpr int kMaxSplitK = 16;   // most row slices of a split-K reduction (nerfhip_sizes.grad_split)
-template <int W, int D>
+template <int W, int D, int NS>
 __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   const int fit = blockIdx.y;
-  const int L = a.fit_layers[fit];
+  const int L = fit_layers_of(a, fit);
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n_params(W, D, L)) return;
   const float* g = a.gpart + fit * a.gp_stride + i;
-  // every slice's load in flight at once (n_split <= kMaxSplitK, uniform):
-  // a runtime-count loop compiled to load → vmcnt(0) → add per slice, 15
-  // serial L2/HBM round trips (10.5 µs of config 2's 93 µs epoch)
-  // (unconditional loads of clamped slices: predicated ones became branches
-  // with a vmcnt(0) drain at every join)
-  float gv[kMaxSplitK];
-  const int ns = a.n_split;
+  // every slice's load in flight at once (NS = n_split, compile-time): a
+  // runtime-count loop compiled to load → vmcnt(0) → add per slice, 15 serial
+  // L2/HBM round trips (10.5 µs of config 2's 93 µs epoch)
+  float gv[NS];
 #pragma unroll
-  for (int sp = 0; sp < kMaxSplitK; ++sp) gv[sp] = g[(sp < ns ? sp : ns - 1) * a.p_stride];
+  for (int sp = 0; sp < NS; ++sp) gv[sp] = g[sp * a.p_stride];
   float gs = gv[0];
 #pragma unroll
-  for (int sp = 1; sp < kMaxSplitK; ++sp) {
-    const float t = gs + gv[sp];
-    gs = sp < ns ? t : gs;             // slice order: the same sum as before
-  }
+  for (int sp = 1; sp < NS; ++sp) gs += gv[sp];   // slice order
   float* P = a.params + fit * a.p_stride;
   float* M = a.m + fit * a.p_stride;
   float* V = a.v + fit * a.p_stride;
@@ -2006,7 +2007,7 @@ __global__ void __launch_bounds__(kNormCols * kNormRowGroups) k_normalize(KArgs 
 // (fp32 precision); wsplit ← both split copies (bf16x3 precision).
 __global__ void k_transpose_params(KArgs a) {
   const int fit = blockIdx.y;
-  const int L = a.fit_layers[fit];
+  const int L = a.fit_layers[fit];   // (prologue: not latency-critical)
   const int W = a.W, D = a.D;
   const int64_t nh = (int64_t)L * W * W, total = nh + (int64_t)W * D;
   const float* P = a.params + fit * a.p_stride;
@@ -2245,6 +2246,21 @@ int launch_rows(const KArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
+// split-K second pass with the slice count compile-time (a power of two,
+// 2..kMaxSplitK: fill_sizes / split_for)
+template <int W, int D>
+int launch_adam_split(const KArgs& a, hipStream_t st) {
+  const dim3 grid((unsigned)((n_params(W, D, a.L_max) + 255) / 256), a.n_fits);
+  switch (a.n_split) {
+    case 2: hipLaunchKernelGGL((k_adam_split<W, D, 2>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((k_adam_split<W, D, 4>), grid, dim3(256), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((k_adam_split<W, D, 8>), grid, dim3(256), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((k_adam_split<W, D, 16>), grid, dim3(256), 0, st, a); break;
+    default: return NERFHIP_ERR_LAUNCH;
+  }
+  return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+
 template <int W, int D, bool X3>
 int launch_params(const KArgs& a, hipStream_t st) {
   if constexpr (X3 && W >= 256) {
@@ -2252,18 +2268,13 @@ int launch_params(const KArgs& a, hipStream_t st) {
       using CS = ParamsCfg<W, D, X3, true>;
       const int grid_s = grid_for(a.n_fits, CS::tiles(a.L_max) * a.n_split);
       hipLaunchKernelGGL((k_step_params<W, D, X3, true>), dim3(grid_s), dim3(CS::THREADS), 0, st, a);
-      const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
-      hipLaunchKernelGGL((k_adam_split<W, D>), dim3(blocks, a.n_fits), dim3(256), 0, st, a);
-      return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+      return launch_adam_split<W, D>(a, st);
     }
   }
   const int grid = grid_for(a.n_fits, ParamsCfg<W, D, X3>::tiles(a.L_max) * a.n_split);
   hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS), 0,
                      st, a);
-  if (a.n_split > 1) {
-    const unsigned blocks = (unsigned)((n_params(W, D, a.L_max) + 255) / 256);
-    hipLaunchKernelGGL((k_adam_split<W, D>), dim3(blocks, a.n_fits), dim3(256), 0, st, a);
-  }
+  if (a.n_split > 1) return launch_adam_split<W, D>(a, st);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
