@@ -111,9 +111,10 @@ typedef struct nerfhip_group {
   float* probe_row_sq;        /* [n][epochs/log_every][n_pad] or NULL          */
   float* grad_partial;        /* [n] optional workspace or NULL.  When set and
                                  n_fits < 8, each epoch's weight gradient is
-                                 reduced in grad_split row slices (partial
-                                 slabs, then a fixed-order sum + Adam): a small
-                                 group otherwise fills only a few workgroups.
+                                 reduced in row slices (partial slabs, then a
+                                 fixed-order sum + Adam): a small group
+                                 otherwise fills only a few workgroups
+                                 (nerfhip_group_plan reports the slices).
                                  Deterministic; slices and tiles depend on the group shape only. */
   void* wsplit;               /* [n] uint16 workspace, BF16X3 only (else NULL):
                                  every weight as exact bf16 split planes, in
