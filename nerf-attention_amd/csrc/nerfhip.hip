@@ -134,8 +134,18 @@ __device__ unsigned long long* g_stamps = nullptr;
       a.pstamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =             \
           __builtin_amdgcn_s_memrealtime();                                            \
   } while (0)
+// the K-split row kernel's stamps, after the parameter kernel's 4096 x 4 x 8
+#define KSTAMP(k)                                                                      \
+  do {                                                                                 \
+    if (a.pstamps && a.mode == 0 && (threadIdx.x & 63) == 0)                           \
+      a.pstamps[131072 + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =    \
+          __builtin_amdgcn_s_memrealtime();                                            \
+  } while (0)
 #else
 #define PSTAMP(k) \
+  do {            \
+  } while (0)
+#define KSTAMP(k) \
   do {            \
   } while (0)
 #define STAMP(k) \
@@ -324,6 +334,21 @@ __host__ __device__ inline int64_t xoff(int R, int K, int r, int k, int plane) {
   return ((((int64_t)(r >> 4) * (K / KC) + k / KC) * 3 + plane) * 16 + (r & 15)) * KC +
          ((k % KC) & ~31) + kperm(k & 31);
 }
+// The K-split row kernel's layout of the same planes (groups that run
+// k_step_rows_ks, KArgs::rows_ks): [R/16][K/32][3 planes][16 rows][32]
+// — every (16-row tile, 32-deep k-slice, plane) is one contiguous 1 KB block,
+// the A-fragment item one wave loads with one fully coalesced 16-B-per-lane
+// load per plane (kperm inside the slice as above).  Read through xoff's
+// [.][K/KC][3][16][KC] chunks, that item was 16 rows x 64 B scattered over 16
+// cache lines: lane-linear items took the K-split row step of one medium fit
+// from 62.2 to 37.3 µs (diagnostic timing, profiles/r03/ks_layout.log).
+__host__ __device__ inline int64_t xoff_ks(int K, int r, int k, int plane) {
+  return ((((int64_t)(r >> 4) * (K >> 5) + (k >> 5)) * 3 + plane) << 9) + ((r & 15) << 5) +
+         kperm(k & 31);
+}
+__host__ __device__ inline int64_t xoff_any(bool ks, int R, int K, int r, int k, int plane) {
+  return ks ? xoff_ks(K, r, k, plane) : xoff(R, K, r, k, plane);
+}
 // per-fit split matrices: forward M_i [out][in] for i = 1..L (hidden) and
 // i = L+1 (final, [D][W]), then the transposed M_iᵀ the backward streams
 __host__ __device__ inline int64_t xs_mat(int W, int D, int L, bool bwd, int i) {
@@ -334,8 +359,8 @@ __host__ __device__ inline int64_t xs_size(int W, int D, int L) {
   return 6 * ((int64_t)L * W * W + (int64_t)D * W);
 }
 // weight element M_i[j][k] = p into both split copies (prologue / split-K)
-__device__ __forceinline__ void put_w(uint16_t* XS, int W, int D, int L, int i, int j, int k,
-                                      float p) {
+__device__ __forceinline__ void put_w(uint16_t* XS, bool ks, int W, int D, int L, int i, int j,
+                                      int k, float p) {
   const int R = i <= L ? W : D;
   uint32_t h, m, l;
   split3(p, h, m, l);
@@ -343,8 +368,8 @@ __device__ __forceinline__ void put_w(uint16_t* XS, int W, int D, int L, int i, 
   const int64_t f = xs_mat(W, D, L, false, i), b = xs_mat(W, D, L, true, i);
 #pragma unroll
   for (int pl = 0; pl < 3; ++pl) {
-    XS[f + xoff(R, W, j, k, pl)] = (uint16_t)part[pl];
-    XS[b + xoff(W, R, k, j, pl)] = (uint16_t)part[pl];
+    XS[f + xoff_any(ks, R, W, j, k, pl)] = (uint16_t)part[pl];
+    XS[b + xoff_any(ks, W, R, k, j, pl)] = (uint16_t)part[pl];
   }
 }
 
@@ -1117,23 +1142,29 @@ __device__ __forceinline__ void ks_stage(float* dst, const float* src, int n, in
 }
 
 // A-fragment item i of a K-deep phase (tile J = i / NM, this wave's k-slice
-// s = w + 4·(i % NM)): three 16-B plane loads of the xoff layout, straight
-// from L2 into registers.
+// s = w + 4·(i % NM)): three plane loads, each one contiguous 1 KB block of
+// the xoff_ks layout (16 B per lane), straight from L2 into registers.
 template <int K> struct KsPhase {
-  static constexpr int KC = kc_of(K), NH = K / KC, KT = KC / 32, NM = K / 128;
-  static_assert(KT >= 4 && K % 128 == 0, "K-split needs K >= 128");
+  static constexpr int NS = K / 32, NM = K / 128;
+  static_assert(K % 128 == 0, "K-split needs K % 128 == 0");
   __amdgpu_buffer_rsrc_t rsrc;
   int voff;
+  // lane (row c, k-group g) of wave w: its 16 B of the 1 KB (tile, slice
+  // w + 4m, plane) block of the xoff_ks layout
   __device__ __forceinline__ KsPhase(const uint16_t* src, int c, int g, int w)
       : rsrc(__builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000)),
-        voff(2 * (c * KC + 8 * g + 32 * w)) {}
+#ifdef NERFHIP_EXP_KS_LINEAR   // diagnostic (timing only): lane-linear offsets
+        voff(16 * (c + 16 * g) + 3072 * w) {}
+#else
+        voff(64 * c + 16 * g + 3072 * w) {}
+#endif
   template <int I> __device__ __forceinline__ S8 load() const {
     constexpr int J = I / NM, m = I % NM;
-    constexpr int base = (J * NH + (4 * m) / KT) * 3 * 16 * KC + 32 * ((4 * m) % KT);
+    constexpr int base = (J * NS + 4 * m) * 3 * 512;     // plane 0 of slice 4m (+ w: voff)
     S8 r;
     r.h = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * base, 0);
-    r.m = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 16 * KC), 0);
-    r.l = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 32 * KC), 0);
+    r.m = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 512), 0);
+    r.l = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 1024), 0);
     return r;
   }
 };
@@ -1276,6 +1307,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   };
   auto no_pre = [](int) { return 0.f; };
   S8 ring[PD];                               // A-fragment items in flight
+  KSTAMP(0);
   ks_prefetch<W>(ring, XS + xs_mat(W, D, L, false, 1), c, g, w);
 
   // ---- layer 0 (K = 1, VALU): this wave's tiles J = 2s + h, s = w + 4m
@@ -1301,6 +1333,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   }
   split_out(ic<W / 128>);
   __syncthreads();
+  KSTAMP(1);
 
   // ---- hidden SineLayers 1..L
   for (int i = 1; i <= L; ++i) {
@@ -1325,6 +1358,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   }
 
   // ---- final nn.Linear(W, D), MSE, dL/dŷ
+  KSTAMP(2);
   ks_stage(bias, P + off_final_w(W, L) + W * D, D, tid);
   const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + fe;
   float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + fe : nullptr;
@@ -1348,6 +1382,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
         return gv;
       },
       own);
+  KSTAMP(3);
   if (!train_f) return;
   sq = wave_sum(sq);
   if (lane == 0) lsum[w] = sq;
@@ -1370,8 +1405,10 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
     split_out(ic<W / 128>);
   };
   bwd(XS + xs_mat(W, D, L, true, L + 1), ys, L, XS + xs_mat(W, D, L, true, L));   // W_fᵀ [W][D]
+  KSTAMP(4);
   for (int i = L; i >= 2; --i)
     bwd(XS + xs_mat(W, D, L, true, i), hs, i - 1, XS + xs_mat(W, D, L, true, i - 1));
+  KSTAMP(5);
   // layer 0: cos(ω(x·w0 + b0)) recomputed; dZ0 reduced over the 16 rows at once
   ks_stage(bias, P, 2 * W, tid);
   float* PZ = SZ + (int64_t)rblk * 2 * W;
@@ -1399,6 +1436,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   if (tid == 0)
     a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] =
         ((lsum[0] + lsum[1]) + lsum[2]) + lsum[3];
+  KSTAMP(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -1604,7 +1642,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // transposed fp32 copy, both split copies of the weights for the row kernel.
 constexpr int kFx = 24;
 
-template <int TJ, int TK, int NW, int WW, int OD>
+template <int TJ, int TK, int NW, int WW, int OD, bool KSX>
 __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
                                            const float* __restrict__ B, int FB, int j0, int k0,
                                            int rb0, int n_blocks, float* G, float* P, float* M,
@@ -1624,6 +1662,10 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   // runtime integer divisions in the Adam epilogue (parameter kernel −0.8 %,
   // 200-epoch sweep +0.5 %, profiles/r02/ab_params_ct_width.log)
   constexpr int W = WW, kOD = OD;
+  // KSX: the split copies go out in the K-split row kernel's layout
+  // (xoff_ks).  Compile-time: a runtime layout select here put the epilogue's
+  // staging arrays in scratch (576 B/lane) and made the W = 512 parameter
+  // kernel 7x slower.
   (void)a;
   (void)out_dim;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1756,9 +1798,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           split3(p, th[qq], tm[qq], tl[qq]);
 #ifndef NERFHIP_EXP_NO_FWDCOPY   // diagnostic build only: timing of the copy's stores
           // forward copy M[j][kcol] of [out_dim][W]
-          XS[xf + xoff(kOD, W, j, kcol, 0)] = (uint16_t)(th[qq] >> 16);
-          XS[xf + xoff(kOD, W, j, kcol, 1)] = (uint16_t)(tm[qq] >> 16);
-          XS[xf + xoff(kOD, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
+          XS[xf + xoff_any(KSX, kOD, W, j, kcol, 0)] = (uint16_t)(th[qq] >> 16);
+          XS[xf + xoff_any(KSX, kOD, W, j, kcol, 1)] = (uint16_t)(tm[qq] >> 16);
+          XS[xf + xoff_any(KSX, kOD, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
 #endif
         }
         if (!G) {   // transposed copy: Mᵀ[kcol][j..j+3] is one 8-B run per plane
@@ -1766,9 +1808,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           const u2 vh = {pk_top(th[0], th[1]), pk_top(th[2], th[3])};
           const u2 vm = {pk_top(tm[0], tm[1]), pk_top(tm[2], tm[3])};
           const u2 vl = {pk_top(tl[0], tl[1]), pk_top(tl[2], tl[3])};
-          *reinterpret_cast<u2*>(XS + xb + xoff(W, kOD, kcol, jb, 0)) = vh;
-          *reinterpret_cast<u2*>(XS + xb + xoff(W, kOD, kcol, jb, 1)) = vm;
-          *reinterpret_cast<u2*>(XS + xb + xoff(W, kOD, kcol, jb, 2)) = vl;
+          *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 0)) = vh;
+          *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 1)) = vm;
+          *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 2)) = vl;
         }
       }
     }
@@ -1813,7 +1855,7 @@ template <int W, int D, bool X3, bool SMALL = false> struct ParamsCfg {
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
-template <int W, int D, bool X3, bool SMALL = false>
+template <int W, int D, bool X3, bool SMALL = false, bool KSX = false>
 __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
                                   (ParamsCfg<W, D, X3, SMALL>::MINB))
     k_step_params(KArgs a) {
@@ -1849,7 +1891,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
     if constexpr (X3)
-      dw_tile_x3<C::T, C::TK, C::NW, W, W>(a, SZ + (int64_t)layer * WN, W,
+      dw_tile_x3<C::T, C::TK, C::NW, W, W, KSX>(a, SZ + (int64_t)layer * WN, W,
                                      SH + (int64_t)(layer - 1) * WN, W, (u / C::NTK) * C::T,
                                      (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
                                      pw + (int64_t)W * W, xs_mat(W, D, L, false, layer),
@@ -1864,7 +1906,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
     if constexpr (X3)
-      dw_tile_x3<C::TD, C::TK, C::NW, W, D>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
+      dw_tile_x3<C::TD, C::TK, C::NW, W, D, KSX>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
                                       (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
                                       pw + (int64_t)W * D, xs_mat(W, D, L, false, L + 1),
                                       xs_mat(W, D, L, true, L + 1), D, (u % C::NTK) == 0,
@@ -1941,14 +1983,14 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   if (i >= fw) {                                       // Wf [D][W] → Wfᵀ [W][D]
     const int64_t r = i - fw;
     if (r < (int64_t)D * W) {
-      if (XS) put_w(XS, W, D, L, L + 1, (int)(r / W), (int)(r % W), p);
+      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, L + 1, (int)(r / W), (int)(r % W), p);
       else PT[(int64_t)L * W * W + (r % W) * D + r / W] = p;
     }
   } else if (i >= 2 * W) {                             // Wi [W][W] → Wiᵀ
     const int64_t r = (i - 2 * W) % ((int64_t)W * W + W);
     const int64_t layer = (i - 2 * W) / ((int64_t)W * W + W);
     if (r < (int64_t)W * W) {
-      if (XS) put_w(XS, W, D, L, (int)layer + 1, (int)(r / W), (int)(r % W), p);
+      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, (int)layer + 1, (int)(r / W), (int)(r % W), p);
       else PT[layer * W * W + (r % W) * W + r / W] = p;
     }
   }
@@ -2020,13 +2062,13 @@ __global__ void k_transpose_params(KArgs a) {
       const int64_t k = u / W, j = u % W;  // PT_i[k][j] = W_i[j][k]
       const float p = P[off_hidden_w(W, (int)i + 1) + j * W + k];
       if (PT) PT[e] = p;
-      if (XS) put_w(XS, W, D, L, (int)i + 1, (int)j, (int)k, p);
+      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, (int)i + 1, (int)j, (int)k, p);
     } else {
       const int64_t u = e - nh;
       const int64_t k = u / D, j = u % D;  // WfT[k][j] = Wf[j][k]
       const float p = P[off_final_w(W, L) + j * W + k];
       if (PT) PT[e] = p;
-      if (XS) put_w(XS, W, D, L, L + 1, (int)j, (int)k, p);
+      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, L + 1, (int)j, (int)k, p);
     }
   }
 }
@@ -2272,6 +2314,13 @@ int launch_params(const KArgs& a, hipStream_t st) {
     }
   }
   const int grid = grid_for(a.n_fits, ParamsCfg<W, D, X3>::tiles(a.L_max) * a.n_split);
+  if constexpr (X3) {
+    if (a.rows_ks && a.n_split == 1) {   // fused epilogue writes the K-split layout
+      hipLaunchKernelGGL((k_step_params<W, D, X3, false, true>), dim3(grid),
+                         dim3(ParamsCfg<W, D, X3>::THREADS), 0, st, a);
+      return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+    }
+  }
   hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS), 0,
                      st, a);
   if (a.n_split > 1) return launch_adam_split<W, D>(a, st);
@@ -2458,6 +2507,11 @@ int epoch_step(GroupRun& r, int e, hipEvent_t* ev /* 3 or NULL */) {
   }
   if (ev) (void)hipEventRecord(ev[0], r.st);
   int rc = r.rows(a, r.st);
+#ifdef NERFHIP_DIAG_ROWS_TWICE
+  // diagnostic build only: the row step again (same inputs, same outputs) with
+  // its weight planes now resident in L2 — how much of it is cold weight reads
+  if (rc == NERFHIP_OK) rc = r.rows(a, r.st);
+#endif
   if (ev) (void)hipEventRecord(ev[1], r.st);
   if (rc == NERFHIP_OK) rc = r.params(a, r.st);
   if (ev) (void)hipEventRecord(ev[2], r.st);

@@ -119,5 +119,10 @@ def test_group_plan(lib):
     assert p.rows_workgroups == 8 * 32 * 5                            # XCD map: 40 fits x 32
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=0)
     assert rc == 0 and p.rows_variant == 0                            # fp32: regular rows
+    # five wide fits at 512 without the workspace (the engine gives none to
+    # 5 x 44 tiles): K-split rows, fused parameter step (k_step_params KSX)
+    rc, p = _plan(lib, W=512, D=128, N=512, n_fits=5, L_max=2, epochs=2000, precision=1)
+    assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (1, 1, 2)
+    assert p.rows_workgroups == 5 * 512 // 16
     assert _plan(lib, W=100, D=128, N=64, n_fits=1, L_max=1, epochs=1)[0] == -1
     assert lib.nerfhip_group_plan(None, None) == -5
