@@ -2198,15 +2198,21 @@ int32_t split_for(const nerfhip_group* g, const nerfhip_sizes& s, bool* small_ti
 // fit 4x the waves and a quarter of the serial GEMM chain per wave, at 4x the
 // weight reads per row and one barrier per output tile: it pays only while the
 // regular kernel leaves most CUs idle, i.e. for groups whose regular grid
-// (n_fits · n_pad/64 workgroups) is at most kKsMaxWorkgroups, so that the
-// K-split grid (4x) runs in one round at one workgroup per CU.  Measured (rows
+// (n_fits · n_pad/64 workgroups) is at most kKsMaxWorkgroups.  Measured (rows
 // kernel, bf16x3, medium): one fit at 1024 / 2048 / 4096 (16 / 32 / 64 regular
 // workgroups) 0.093 → 0.066 ms each; two fits at 2048 (64) 0.093 → 0.068;
 // three fits (96) 0.093 → 0.125; 8 fits 0.096 → 0.254; 5 large fits 0.29 →
 // 0.62; one wide fit at 8192 (128) 0.36 → 0.59; one large fit at 2048 (32)
-// 0.256 → 0.201 (profiles/r02/ks_threshold.log).  NERFHIP_ROWS_KS = 0 / 1 forces the choice
+// 0.256 → 0.201 (profiles/r02/ks_threshold.log).  With the xoff_ks weight
+// layout (round 3) the K-split kernel also wins at 128 regular workgroups
+// (4 x 128 K-split workgroups, two rounds at one per CU), whole epochs of
+// 200-epoch runs: one medium fit at 8192 0.139 → 0.133 ms, one wide fit at
+// 8192 (config 5) 0.463 → 0.434, two medium at 4096 0.134 → 0.129, four at
+// 2048 0.140 → 0.135, eight at 1024 0.180 → 0.168, sixteen at 512 0.159 →
+// 0.148; at 256 it loses (eight medium at 2048 0.225 → 0.288;
+// profiles/r03/ks_crossover.log).  NERFHIP_ROWS_KS = 0 / 1 forces the choice
 // (supported shapes only: bf16x3, W >= 128, D = 128).
-constexpr int64_t kKsMaxWorkgroups = 64;
+constexpr int64_t kKsMaxWorkgroups = 128;
 bool rows_ks_for(const nerfhip_group* g, const nerfhip_sizes& s) {
   if (g->precision != NERFHIP_PRECISION_BF16X3 || g->W < 128 || g->D != 128) return false;
   const char* e = getenv("NERFHIP_ROWS_KS");
@@ -2261,9 +2267,9 @@ int launch_rows(const KArgs& a, hipStream_t st) {
       // every final tile are wrong in a bad block); this single runtime-mode
       // kernel measured correct with and without sharing, and
       // tests/test_gpu_parity.py::test_rows_ks_coresident pins that.  The
-      // cause was not isolated, so the kernel keeps a CU to itself; below
-      // kKsMaxWorkgroups the grid is under the CU count and the padding costs
-      // nothing.  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics only) drops the
+      // cause was not isolated, so the kernel keeps a CU to itself: up to 64
+      // regular workgroups the grid fits the 256 CUs, up to kKsMaxWorkgroups
+      // (128) it takes two rounds (still faster, rows_ks_for).  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics only) drops the
       // padding so that two workgroups may share a CU.
       const char* e = getenv("NERFHIP_KS_SHARE_CU");
       const unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;

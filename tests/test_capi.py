@@ -102,7 +102,8 @@ def test_group_plan(lib):
     """nerfhip_group_plan (host only): BASELINE config 2, one medium fit at
     seq 2048 in bf16x3 with the split-K workspace, takes the K-split row kernel
     (one 16-row block per workgroup) and 8 gradient row slices on 64 x 64
-    tiles; a wide fit at 8192 128 x 128 tiles x 8 slices; a 40-fit
+    tiles; a wide fit at 8192 (128 regular workgroups) K-split rows too and
+    128 x 128 tiles x 8 slices; a 40-fit
     sweep chunk the regular kernels, fused."""
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=1,
                   grad_partial=1)
@@ -112,7 +113,7 @@ def test_group_plan(lib):
     assert p.launches_per_epoch == 3
     rc, p = _plan(lib, W=512, D=128, N=8192, n_fits=1, L_max=3, epochs=2000, precision=1,
                   grad_partial=1)
-    assert rc == 0 and (p.rows_variant, p.grad_split) == (0, 8)
+    assert rc == 0 and (p.rows_variant, p.grad_split) == (1, 8)       # 128 regular -> K-split
     assert p.params_workgroups == 8 * (3 * 16 + 1 * 4 + 512 // 64)     # 60 128x128 tiles
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=40, L_max=3, epochs=2000, precision=1)
     assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (0, 1, 2)
