@@ -168,6 +168,14 @@ __device__ __forceinline__ void sst(float* p, float v) { __builtin_nontemporal_s
 __device__ __forceinline__ void sst4(float* p, f4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
 }
+// the row kernel's private cos(ωz) tiles (stored in the forward, re-read by
+// the same workgroup's backward): NERFHIP_COS_NT=0 stores them L2-allocating
+#ifndef NERFHIP_COS_NT
+#define NERFHIP_COS_NT 1
+#endif
+__device__ __forceinline__ void cst4(float* p, f4 v) {
+  if constexpr (NERFHIP_COS_NT) sst4(p, v); else st4(p, v);
+}
 
 template <int CTRL> __device__ __forceinline__ float dpp_quad(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
@@ -973,7 +981,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
         },
         [&](int J) {
           if (train) {
-            sst4(SCi + J * 256, cs_pend);
+            cst4(SCi + J * 256, cs_pend);
             tile_store(SHti, SHi, J, ho[J % JP]);
           }
         });
