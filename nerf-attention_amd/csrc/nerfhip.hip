@@ -1114,7 +1114,13 @@ template <int W> struct KsCfg {
   // A-fragment items (S8) in flight per wave.  (W = 256: 10 and 12 items
   // measured 3.5 % and 7 % slower than 6 on one medium fit: not load-latency
   // bound, profiles/r02/ab_ks_prefetch_depth.log)
-  static constexpr int PD = W >= 512 ? 8 : 6;
+#ifndef NERFHIP_KS_PD256
+#define NERFHIP_KS_PD256 6
+#endif
+#ifndef NERFHIP_KS_PD512
+#define NERFHIP_KS_PD512 8
+#endif
+  static constexpr int PD = W >= 512 ? NERFHIP_KS_PD512 : NERFHIP_KS_PD256;
 };
 __host__ __device__ constexpr int ks_owner(int J) { return (J >> 1) & 3; }
 __host__ __device__ constexpr int ks_local(int J) { return 2 * (J >> 3) + (J & 1); }
