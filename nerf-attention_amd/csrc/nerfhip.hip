@@ -1993,6 +1993,9 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   P[i] = p; M[i] = mm; V[i] = vv;
   float* PT = a.params_t + fit * a.pt_stride;
   uint16_t* XS = a.x3 ? a.wsplit + fit * a.ws_stride : nullptr;
+#ifdef NERFHIP_EXP_ADAM_NO_SPLIT_COPIES   // diagnostic (wrong results): cost of the split-copy stores
+  if (XS) return;
+#endif
   const int64_t fw = off_final_w(W, L);
   if (i >= fw) {                                       // Wf [D][W] → Wfᵀ [W][D]
     const int64_t r = i - fw;
