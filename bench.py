@@ -214,21 +214,44 @@ def e2e_fit_kv_cache(seq_len: int, epochs: int, precision: str) -> dict:
             "note": "whole fit_kv_cache call incl. loads, inits, D2H, checkpoints and JSON"}
 
 
-def isolated_kernel(gspecs, kname, flops, precision, peak, device, epochs=41) -> dict:
-    """The dominant kernel's group trained alone (no concurrent groups) for a
-    few epochs, after the timed region: its undisturbed launch time (every
-    4th epoch timed from epoch 3, so 10 launches at 41 epochs and never the
-    cold first one)."""
+ISO_EPOCHS = 101   # isolated leg: 25 timed launches (every 4th epoch from epoch 3)
+# the committed rocprofv3 summary of exactly that leg (tools/r4/iso_prof.sh runs
+# tools/r4/isokernel.py, which calls isolated_kernel below, under
+# rocprofv3 --kernel-trace --stats, and its PMC passes)
+ISO_PROFILE = "profiles/r04/rocprof_kernel_stats_isolated_rows256.csv"
+ISO_PMC = ROOT / "profiles" / "r04" / "pmc_isolated_rows256.json"
+
+
+def heaviest_group(specs, width: int, device: int = 0) -> list:
+    """Indices (into `specs`) of the engine's heaviest group of hidden width
+    `width`, exactly as engine.plan_groups chunks the job (the sweep's W = 256
+    group: the first of four 40-fit chunks)."""
+    from nerf_attention import engine
+    for _d, members in engine.plan_groups(specs, device):
+        if specs[members[0]].config.hidden_features == width:
+            return list(members)
+    raise ValueError(f"no group of width {width}")
+
+
+def isolated_kernel(gspecs, kname, flops, precision, peak, device,
+                    epochs=ISO_EPOCHS) -> dict:
+    """The dominant kernel's group trained alone (no concurrent groups) for
+    `epochs` epochs: its undisturbed launch time (hipEvents around every 4th
+    epoch's launches from epoch 3, so never the cold first one)."""
     from nerf_attention import engine
     job = engine.FitJob(gspecs, epochs, devices=[device], precision=precision)
     job.launch(timed=True)
     job.wait()
     t = job.timing[0]
+    if t.launches == 0:
+        raise ValueError(f"isolated leg needs >= 4 epochs (got {epochs}): no timed launch")
     ms = (t.rows_ms if "rows" in kname else t.params_ms) / t.launches
+    other_ms = (t.params_ms if "rows" in kname else t.rows_ms) / t.launches
     tf = flops / (ms * 1e-3) / 1e12
     return {"avg_launch_ms": round(ms, 4), "achieved": round(tf, 2), "frac": round(tf / peak, 4),
             "frac_of_f32_mfma_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "epochs": epochs,
-            "launches": t.launches}
+            "launches": t.launches, "partner_kernel_avg_ms": round(other_ms, 4),
+            "epoch_ms": round(job.group_seconds()[0] * 1e3 / epochs, 4)}
 
 
 def fp32_sweep(specs, epochs, device, plan, ref_cos, n_total) -> dict:
@@ -397,29 +420,46 @@ def main() -> None:
                 # PMC bytes per launch (separate, serialised rocprofv3 passes of the
                 # same workload, tools/profile_round.sh) over this run's launch time
                 hbm = traffic["bytes"] / (avg_ms * 1e-3) / 1e9
-            gcf = [specs[mine[i]].config for i in g.members]
+            # the isolated leg: the engine's heaviest group of the dominant width
+            # (deterministic, the same group tools/r4/isokernel.py profiles)
+            my_specs = [specs[i] for i in mine]
+            gw = int(kname.split("<")[1].split(",")[0])
+            gsel = heaviest_group(my_specs, gw, local)
+            gcf = [my_specs[i].config for i in gsel]
             g_flops = (rows_flops if "rows" in kname else params_flops)(N, 128, gcf)
             progress(f"isolated {kname}")
-            iso = isolated_kernel([specs[mine[i]] for i in g.members], kname, g_flops,
+            iso = isolated_kernel([my_specs[i] for i in gsel], kname, g_flops,
                                   args.precision, peak, local)
-            iso["fits"] = g.n
-            hbm_iso = traffic and traffic["bytes"] / (iso["avg_launch_ms"] * 1e-3) / 1e9
+            iso["fits"] = len(gsel)
+            iso_pmc = None
+            if ISO_PMC.exists():
+                iso_pmc = json.loads(ISO_PMC.read_text()).get(f"{kname}[{args.precision}]")
+            iso_bytes = iso_pmc and iso_pmc["bytes"]
+            hbm_iso = iso_bytes and iso_bytes / (iso["avg_launch_ms"] * 1e-3) / 1e9
             roof = {"bound": "mfma", "achieved": iso["achieved"],
                     "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": iso["frac"],
-                    "frac_kind": "dominant kernel on its heaviest group, timed alone right after "
-                                 "the timed region: algorithmic FLOPs per launch / mean hipEvent "
-                                 "launch duration (10 launches, cold first launch excluded)",
+                    "frac_kind": "dominant kernel on the engine's heaviest group of its width, "
+                                 "timed alone right after the timed region: algorithmic FLOPs "
+                                 f"per launch / mean hipEvent launch duration ({iso['launches']} "
+                                 f"launches of {iso['epochs']} epochs, cold first launch "
+                                 "excluded)",
                     "avg_launch_ms": iso["avg_launch_ms"], "flops_per_launch": g_flops,
-                    "fits_per_launch": g.n,
-                    "traffic": traffic and traffic["bytes"],
-                    "traffic_detail": traffic,
-                    "mfma_busy": traffic and traffic.get("mfma_busy"),
+                    "fits_per_launch": len(gsel),
+                    "rocprof_isolated": ISO_PROFILE,
+                    "rocprof_isolated_avg_ms": iso_pmc and iso_pmc.get("rocprof_avg_ms"),
+                    "traffic": iso_bytes,
+                    "traffic_detail": iso_pmc,
+                    "traffic_source": "rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of the "
+                                      "same isolated group (tools/r4/iso_prof.sh, "
+                                      "profiles/r04/pmc_isolated_rows256.json)",
+                    "mfma_busy": iso_pmc and iso_pmc.get("mfma_busy"),
                     "mfma_busy_kind": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GPU-active "
-                                      "cycles), rocprofv3 PMC pass of the sweep (dispatches "
-                                      "serialised)",
+                                      "cycles), rocprofv3 PMC pass of the same isolated group",
                     "hbm_gbs": hbm_iso and round(hbm_iso, 1),
                     "hbm_frac": hbm_iso and round(hbm_iso / HBM_PEAK_GBS, 4),
+                    "sweep_context_traffic": traffic and traffic["bytes"],
+                    "sweep_context_mfma_busy": traffic and traffic.get("mfma_busy"),
                     "kernel": f"{kname} [{args.precision}]",
                     "flops_unit": "algorithmic fp32 GEMM FLOPs (2 per multiply-add), "
                                   "SURVEY.md §8d",

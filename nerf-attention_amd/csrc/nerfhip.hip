@@ -218,7 +218,36 @@ __device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
 // class as the SLEEF kernels ATen uses on CPU).  Kept branch-free and short:
 // the OCML sincosf carries a Payne–Hanek path whose registers spill the
 // W ≥ 256 step kernels.
+#ifndef NERFHIP_SINCOS
+#define NERFHIP_SINCOS 0
+#endif
 __device__ __forceinline__ void sincos_fast(float x, float* s_out, float* c_out) {
+#if NERFHIP_SINCOS == 1
+  // Cody–Waite by π (C1, C2 with 12 trailing zero bits: n·C exact for
+  // |n| < 2^12), u = r/(2π) ∈ [−1/4, 1/4] revolutions, the hardware
+  // v_sin_f32 / v_cos_f32, and the sign (−1)^n as a sign-bit xor
+  {
+    const float n = __builtin_rintf(x * 0.318309873342514038086f);
+    float r = fmaf(n, -3.14062500000000000000e+00f, x);
+    r = fmaf(n, -9.67502593994140625000e-04f, r);
+    r = fmaf(n, -1.50995802528086642269e-07f, r);
+    const float u = r * 0.159154936671257019043f;
+    const uint32_t sg = (uint32_t)(int)n << 31;
+    *s_out = __uint_as_float(__float_as_uint(__builtin_amdgcn_sinf(u)) ^ sg);
+    *c_out = __uint_as_float(__float_as_uint(__builtin_amdgcn_cosf(u)) ^ sg);
+    return;
+  }
+#elif NERFHIP_SINCOS == 2
+  // reduction in revolutions (1/2π = hi + lo), the hardware v_sin / v_cos
+  {
+    const float n = __builtin_rintf(x * 0.159154936671257019043f);
+    float u = fmaf(x, 0.159154936671257019043f, -n);
+    u = fmaf(x, 6.42063824329852650408e-09f, u);
+    *s_out = __builtin_amdgcn_sinf(u);
+    *c_out = __builtin_amdgcn_cosf(u);
+    return;
+  }
+#endif
   const float n = __builtin_rintf(x * 0.636619772367581343f);
   float r = fmaf(n, -1.57079601287841796875f, x);
   r = fmaf(n, -3.13916912752797361463e-07f, r);

@@ -186,6 +186,34 @@ def make_wide():
     (HERE / "wide_8192_e30.json").write_text(json.dumps(out, indent=1))
 
 
+def make_wide_full():
+    """BASELINE config 5 at its stated length: (512,3) at N=8192, 2000 epochs,
+    the reference's own fit_siren (siren.py:70-149) under manual_seed(0) on the
+    reference's synthetic layer-0 key head 0 (extract.py:182-259)."""
+    siren, types, extract, _ = _ref()
+    d = SCRATCH / "kv_8192_l1"
+    if not (d / "layer_00.pt").exists():
+        with contextlib.redirect_stdout(io.StringIO()):
+            extract.extract_kv_cache_synthetic(seq_len=8192, num_layers=1, num_kv_heads=1,
+                                               head_dim=128, output_dir=d)
+    x = torch.load(d / "layer_00.pt", weights_only=True)["keys"][0]
+    torch.manual_seed(0)
+    t0 = time.time()
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        r = siren.fit_siren(x, types.SIRENConfig(*WIDE), epochs=2000, device="cpu",
+                            log_every=500, verbose=True)
+    out = {"target_sha256": sha(x.numpy()), "epochs": 2000, "losses": r.losses,
+           "final_mse": r.final_mse, "final_cosine_mean": r.final_cosine_mean,
+           "final_cosine_min": r.final_cosine_min, "final_cosine_std": r.final_cosine_std,
+           "cosine_sims_every64": r.cosine_sims[::64].tolist(),
+           "log_lines": buf.getvalue().splitlines(),
+           "params_sha256": sha(flat_state(r.model)),
+           "train_time_seconds_cpu": time.time() - t0, "threads": torch.get_num_threads(),
+           "torch": torch.__version__}
+    (HERE / "wide_8192_e2000.json").write_text(json.dumps(out, indent=1))
+
+
 SCAN_LENGTHS = (512, 1024, 4096)
 
 

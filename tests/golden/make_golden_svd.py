@@ -19,6 +19,7 @@ import contextlib
 import io
 import json
 import os
+import sys
 import tempfile
 from pathlib import Path
 
@@ -32,7 +33,11 @@ def main():
     from nerf_attention.experiments import svd
     assert "/root/reference" in os.path.abspath(svd.__file__), svd.__file__
     torch.set_num_threads(8)
-    for tag, shape in (("q512", (512, 4, 4, 128)), ("s2048", (2048, 32, 8, 128))):
+    shapes = {"q512": (512, 4, 4, 128), "s2048": (2048, 32, 8, 128),
+              # BASELINE config 5's SVD leg: the Llama shape at seq_len 8192
+              "s8192": (8192, 32, 8, 128)}
+    tags = sys.argv[1:] or ["q512", "s2048"]
+    for tag, shape in ((t, shapes[t]) for t in tags):
         with tempfile.TemporaryDirectory() as tmp:
             kv, out = Path(tmp) / "kv", Path(tmp) / "svd"
             n, layers, heads, d = shape

@@ -20,7 +20,7 @@ import torch
 from nerf_attention import SIREN, SIRENConfig, engine
 from nerf_attention.synthetic import kv_slice
 
-os.environ["NERFHIP_ROWS_KS"] = "1"
+os.environ["NERFHIP_ROWS_KS"] = os.environ.get("ROWS_KS", "1")   # 0: the regular row kernel
 tag = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 cases = [(256, 2, 8192, 0), (256, 2, 8192, 3), (512, 3, 8192, 0), (256, 2, 16384, 0),
