@@ -36,12 +36,12 @@ def _slices(g):
     return out
 
 
-@pytest.mark.parametrize("tag", ["q512", "s2048"])
+@pytest.mark.parametrize("tag", ["q512", "s2048", "s8192"])
 def test_oracle_matches_reference(golden_dir, tag):
     g = _golden(golden_dir, tag)
     sl = _slices(g)
     torch.set_num_threads(8)
-    for rec in g["records"][:: (1 if tag == "q512" else 3)]:
+    for rec in g["records"][:: {"q512": 1, "s2048": 3, "s8192": 7}[tag]]:
         t = sl[(rec["layer"], rec["head"], rec["kv_type"])]
         assert svd_rank(rec["seq_len"], rec["d_head"], rec["target_compression"]) == rec["rank"]
         m = svd_oracle.slice_metrics(t, rec["rank"])
@@ -57,8 +57,10 @@ def test_record_arithmetic(golden_dir):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["q512", "s2048"])
+@pytest.mark.parametrize("tag", ["q512", "s2048", "s8192"])
 def test_engine_matches_reference(gpu, golden_dir, tag):
+    """s8192: BASELINE config 5's SVD leg (experiments/svd.py:48-57 at the
+    Llama shape, seq_len 8192), tests/golden/make_golden_svd.py s8192."""
     from nerf_attention.svd import rank_metrics
     g = _golden(golden_dir, tag)
     sl = _slices(g)
