@@ -121,8 +121,8 @@ def cgroup_throttled_us() -> int | None:
     return None
 
 
-def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
-                 warmup_epochs: int = 10, sample_s: float | None = 0.6) -> dict:
+def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 3,
+                 warmup_epochs: int = 10, sample_s: float | None = 2.0) -> dict:
     """Time the package's own host path (host_fit.fit_on_host: the reference
     loop, siren.py:80-149, in eager PyTorch) on every architecture: one untimed
     warm-up fit of `warmup_epochs` per architecture (thread pool, allocator,
@@ -164,8 +164,12 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
         torch.set_num_threads(prev)
     per_epoch = {k: float(np.median(v)) for k, v in samples.items()}
     sweep_s = 40 * 2000 * sum(per_epoch.values())
-    # spread of the repeats around the median, worst architecture
-    spread = max((max(v) - min(v)) / float(np.median(v)) for v in samples.values())
+    # spread of the repeats around the median: worst architecture, and weighted
+    # by each architecture's share of the extrapolated sweep time
+    spread_of = {k: (max(v) - min(v)) / float(np.median(v)) for k, v in samples.items()}
+    spread = max(spread_of.values())
+    tot = sum(per_epoch.values())
+    spread_w = sum(spread_of[k] * per_epoch[k] / tot for k in per_epoch)
     timed_s = sum(epochs_of[k] * sum(v) for k, v in samples.items())
     thr1 = cgroup_throttled_us()
     cpus["throttled_s_during_baseline"] = (thr1 - thr0) / 1e6 if thr0 is not None and thr1 is not None \
@@ -182,6 +186,9 @@ def cpu_baseline(seq_len: int, sample_epochs: int, repeats: int = 5,
                       f"cgroup quota {cpus['cgroup_cpu_quota']})",
             "host": cpus, "repeat_spread": round(spread, 4),
             "repeat_spread_kind": "(max - min) / median of the timed repeats, worst arch",
+            "repeat_spread_weighted": round(spread_w, 4),
+            "repeat_spread_weighted_kind": "per-arch (max - min) / median weighted by the arch's "
+                                           "share of the extrapolated sweep time",
             "per_epoch_ms": {k: round(v * 1e3, 3) for k, v in per_epoch.items()},
             "spread_per_arch": {k: round((max(v) - min(v)) / float(np.median(v)), 4)
                                 for k, v in samples.items()}}
@@ -254,17 +261,28 @@ def isolated_kernel(gspecs, kname, flops, precision, peak, device,
             "epoch_ms": round(job.group_seconds()[0] * 1e3 / epochs, 4)}
 
 
-def fp32_sweep(specs, epochs, device, plan, ref_cos, n_total) -> dict:
-    """One timed sweep on the exact f32 MFMA path (same fits, same parity bar)."""
+def fp32_sweep(specs, epochs, device, plan, ref_cos, n_total, warmup: int = 1,
+               steps: int = 3) -> dict:
+    """The exact f32 MFMA path timed under the headline's protocol (same fits,
+    same parity bar): `warmup` untimed sweeps, then `steps` timed sweeps
+    bracketed by device synchronisation."""
     from nerf_attention import engine
     job = engine.FitJob(specs, epochs, devices=[device], precision="fp32")
+    for _ in range(warmup):
+        job.launch()
+        job.wait()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    job.launch()
-    job.wait()
-    dt = time.perf_counter() - t0
+    for _ in range(steps):
+        job.launch()
+        job.wait()
+        progress("fp32 step done")
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
     out = {"value": round(len(specs) / dt, 4), "unit": "fits/s", "ms_per_step": round(dt * 1e3, 2),
-           "note": "one sweep, first launch of this job (no warm-up)"}
+           "warmup": warmup, "steps": steps,
+           "note": f"{warmup} untimed warm-up sweep(s), then {steps} timed sweeps (the headline's "
+                   "protocol)"}
     if ref_cos is not None and GOLDEN_SWEEP.exists():
         ref = {r["name"]: r["final_cosine_mean"]
                for r in json.loads(GOLDEN_SWEEP.read_text())["records"]}

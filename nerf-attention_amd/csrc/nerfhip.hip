@@ -1187,35 +1187,56 @@ __device__ __forceinline__ void ks_stage(float* dst, const float* src, int n, in
 // A-fragment item i of a K-deep phase (tile J = i / NM, this wave's k-slice
 // s = w + 4·(i % NM)): three plane loads, each one contiguous 1 KB block of
 // the xoff_ks layout (16 B per lane), straight from L2 into registers.
+//
+// Every load takes its whole offset from a VGPR (soffset 0, the plane as the
+// 12-bit immediate) and all phases share ONE buffer resource over the fit's
+// split weights (the matrix offset goes into the VGPR too).  Root cause of the
+// K-split co-residency fault: with a compile-time item offset
+// in the instruction's soffset, hipcc materialised it into an SGPR right
+// before each load (s_mov_b32 s2, 0x12000; buffer_load … s2; s_mov_b32 s2,
+// 0x12400; …) and rewrote that SGPR — and the resource SGPRs of a finished
+// phase — one instruction after the load issued.  On gfx950 a vector-memory
+// instruction that waits behind a backed-up memory pipeline reads its SGPR
+// operands late, so under two workgroups per CU some loads fetched the NEXT
+// item's offset (wrong weights, whole 16-row blocks wrong).  Eight wait states
+// between every such load and the SALU write removed the fault
+// (tools/r4/ks_patch.py nopsmov8, profiles/r04/ks_bisect.log); two did not.
+// The compiler models this hazard for gfx10+ only, so the kernel avoids the
+// pattern: the only SGPRs its loads read are the one resource, set once.
 template <int K> struct KsPhase {
   static constexpr int NS = K / 32, NM = K / 128;
   static_assert(K % 128 == 0, "K-split needs K % 128 == 0");
   __amdgpu_buffer_rsrc_t rsrc;
   int voff;
   // lane (row c, k-group g) of wave w: its 16 B of the 1 KB (tile, slice
-  // w + 4m, plane) block of the xoff_ks layout
-  __device__ __forceinline__ KsPhase(const uint16_t* src, int c, int g, int w)
-      : rsrc(__builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000)),
+  // w + 4m, plane) block of the xoff_ks layout; mat: the phase's matrix,
+  // in bf16 elements from the fit's split-weight base xs
+  __device__ __forceinline__ KsPhase(const uint16_t* xs, int mat, int c, int g, int w)
+      : rsrc(__builtin_amdgcn_make_buffer_rsrc((void*)xs, 0, 0x7fffffff, 0x00020000)),
 #ifdef NERFHIP_EXP_KS_LINEAR   // diagnostic (timing only): lane-linear offsets
-        voff(16 * (c + 16 * g) + 3072 * w) {}
+        voff(16 * (c + 16 * g) + 3072 * w + 2 * mat) {}
 #else
-        voff(64 * c + 16 * g + 3072 * w) {}
+        voff(64 * c + 16 * g + 3072 * w + 2 * mat) {}
 #endif
   template <int I> __device__ __forceinline__ S8 load() const {
     constexpr int J = I / NM, m = I % NM;
     constexpr int base = (J * NS + 4 * m) * 3 * 512;     // plane 0 of slice 4m (+ w: voff)
+    // the item's byte offset as a VGPR add the backend cannot split into an
+    // SGPR soffset (see above); planes 1 KB apart fit the immediate field
+    int v;
+    asm("v_add_u32 %0, %1, %2" : "=v"(v) : "i"(2 * base), "v"(voff));
     S8 r;
-    r.h = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * base, 0);
-    r.m = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 512), 0);
-    r.l = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 2 * (base + 1024), 0);
+    r.h = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 0, 0);
+    r.m = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v + 1024, 0, 0);
+    r.l = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v + 2048, 0, 0);
     return r;
   }
 };
 // the first PD items of a phase into the ring (issued a phase ahead)
 template <int K, int PD>
-__device__ __forceinline__ void ks_prefetch(S8 (&ring)[PD], const uint16_t* src, int c, int g,
-                                            int w) {
-  const KsPhase<K> ph(src, c, g, w);
+__device__ __forceinline__ void ks_prefetch(S8 (&ring)[PD], const uint16_t* xs, int mat, int c,
+                                            int g, int w) {
+  const KsPhase<K> ph(xs, mat, c, g, w);
   static_for<0, PD>([&](auto ic_i) {
     constexpr int i = decltype(ic_i)::value;
     ring[i] = ph.template load<i>();
@@ -1230,13 +1251,13 @@ __device__ __forceinline__ void ks_prefetch(S8 (&ring)[PD], const uint16_t* src,
 // pre(J) → a per-lane float loaded one tile ahead of fin; fin(J, acc, pv) →
 // the finalised element (feature 16J+4g+w, row c); own(J, f4) on the owner.
 template <int K, int JT, int PD, int KN, class Pre, class Fin, class Own>
-__device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ src, const S8 (&b)[K / 128],
-                                        S8 (&ring)[PD], const uint16_t* next, int w, int c, int g,
+__device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ xs, int src, const S8 (&b)[K / 128],
+                                        S8 (&ring)[PD], int next, int w, int c, int g,
                                         int lane, float* part, float* outb, Pre&& pre, Fin&& fin,
                                         Own&& own) {
   constexpr int NM = K / 128, NI = JT * NM;
   static_assert(NI >= PD, "phase shorter than the prefetch depth");
-  const KsPhase<K> ph(src, c, g, w);
+  const KsPhase<K> ph(xs, src, c, g, w);
   const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
   // tiles go in pairs, one barrier per pair: LDS slot of tile J = 2·(pair parity) + (J & 1)
   auto slot = [](int J) { return 2 * ((J >> 1) & 1) + (J & 1); };
@@ -1283,7 +1304,7 @@ __device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ src, const 
     }
   });
   if constexpr (KN > 0) {
-    if (next) ks_prefetch<KN>(ring, next, c, g, w);
+    if (next >= 0) ks_prefetch<KN>(ring, xs, next, c, g, w);
   }
   finalize(JT - 2, pv_prev[0]);
   finalize(JT - 1, pv_prev[1]);
@@ -1351,7 +1372,9 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   auto no_pre = [](int) { return 0.f; };
   S8 ring[PD];                               // A-fragment items in flight
   KSTAMP(0);
-  ks_prefetch<W>(ring, XS + xs_mat(W, D, L, false, 1), c, g, w);
+  // matrix offsets of the fit's split weights (bf16 elements; < 2^31 bytes)
+  auto xm = [&](bool bwd_mat, int i) { return (int)xs_mat(W, D, L, bwd_mat, i); };
+  ks_prefetch<W>(ring, XS, xm(false, 1), c, g, w);
 
   // ---- layer 0 (K = 1, VALU): this wave's tiles J = 2s + h, s = w + 4m
   ks_stage(bias, P, 2 * W, tid);
@@ -1384,7 +1407,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
     float* SHi = SH + (int64_t)i * WN + eoff;
     float* SCi = SC + (int64_t)i * WN + coff;
     gemm_ks<W, JW, PD, W>(
-        XS + xs_mat(W, D, L, false, i), hs, ring, XS + xs_mat(W, D, L, false, i + 1), w, c, g,
+        XS, xm(false, i), hs, ring, xm(false, i + 1), w, c, g,
         lane, part, outb, no_pre,
         [&](int J, float acc, float) {
           const float z = __fadd_rn(acc, bias[16 * J + fe]);
@@ -1408,7 +1431,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   float* SGe = SG + (int64_t)rblk * D * 16 + fe * 16 + c;
   float sq = 0.f;
   gemm_ks<W, JD, PD, D>(
-      XS + xs_mat(W, D, L, false, L + 1), hs, ring, train_f ? XS + xs_mat(W, D, L, true, L + 1) : nullptr,
+      XS, xm(false, L + 1), hs, ring, train_f ? xm(true, L + 1) : -1,
       w, c, g,
       lane, part, outb,
       [&](int J) { return train_f ? T[16 * J] : 0.f; },
@@ -1433,12 +1456,12 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 
   // ---- backward: dZ = (dH ⊙ cos(ωz))·ω, stored for the weight gradients
   // (the phase after W_iᵀ is W_{i-1}ᵀ, down to W_1ᵀ: xs_mat(.., true, i - 1))
-  auto bwd = [&](const uint16_t* Mt, const auto& bop, int layer, const uint16_t* next) {
+  auto bwd = [&](int Mt, const auto& bop, int layer, int next) {
     const float* SCl = SC + (int64_t)layer * WN + coff;
     float* SZl = SZ + (int64_t)layer * WN + eoff;
     constexpr int K = (sizeof(bop) / sizeof(bop[0])) * 128;
     gemm_ks<K, JW, PD, W>(
-        Mt, bop, ring, next, w, c, g, lane, part, outb, [SCl](int J) { return SCl[J * 256]; },
+        XS, Mt, bop, ring, next, w, c, g, lane, part, outb, [SCl](int J) { return SCl[J * 256]; },
         [&, SZl](int J, float acc, float cs) {
           const float dz = __fmul_rn(__fmul_rn(acc, cs), om);
           sst(SZl + J * 256, dz);
@@ -1447,16 +1470,16 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
         own);
     split_out(ic<W / 128>);
   };
-  bwd(XS + xs_mat(W, D, L, true, L + 1), ys, L, XS + xs_mat(W, D, L, true, L));   // W_fᵀ [W][D]
+  bwd(xm(true, L + 1), ys, L, xm(true, L));   // W_fᵀ [W][D]
   KSTAMP(4);
   for (int i = L; i >= 2; --i)
-    bwd(XS + xs_mat(W, D, L, true, i), hs, i - 1, XS + xs_mat(W, D, L, true, i - 1));
+    bwd(xm(true, i), hs, i - 1, xm(true, i - 1));
   KSTAMP(5);
   // layer 0: cos(ω(x·w0 + b0)) recomputed; dZ0 reduced over the 16 rows at once
   ks_stage(bias, P, 2 * W, tid);
   float* PZ = SZ + (int64_t)rblk * 2 * W;
   gemm_ks<W, JW, PD, 0>(
-      XS + xs_mat(W, D, L, true, 1), hs, ring, nullptr, w, c, g, lane, part, outb, no_pre,
+      XS, xm(true, 1), hs, ring, -1, w, c, g, lane, part, outb, no_pre,
       [&](int J, float acc, float) {
         const int f = 16 * J + fe;
         const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);

@@ -408,6 +408,99 @@ class FitJob:
         return outs
 
 
+class StreamingJob:
+    """A one-device job whose groups launch as soon as their fits' inputs exist.
+
+    The drop-in driver initialises its models in the reference's RNG order
+    (fit.py:54-69), one after the other on the host; a FitJob would wait for
+    all of them.  Here the group plan is fixed up front from each fit's
+    (config, seq_len, d_head) — `plan_groups` needs nothing else — and
+    `add(i, spec)` hands over fit i's target and init: the moment the last
+    member of a group (a chunk of consecutive reference-order fits of one
+    width) arrives, that group's buffers are packed and its whole training is
+    enqueued on its own stream, while the host goes on drawing the next inits.
+    `finished()` then yields groups in the order they complete, so results,
+    checkpoints and progress lines can be produced while the rest still
+    trains.  Results are bitwise those of a FitJob over the same groups: the
+    grouping is identical and groups never interact."""
+
+    def __init__(self, protos: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
+                 device=None, precision: str | None = None):
+        _native.load()
+        self.precision = check_precision(precision)
+        self.device = resolve_device(torch.device("cuda", device) if device is not None
+                                     else "cuda").index
+        self.epochs, self.lr, self.log_every = epochs, lr, log_every
+        self.protos = protos
+        self.plan = plan_groups(protos, self.device)
+        self.member_of = {i: gi for gi, (_d, m) in enumerate(self.plan) for i in m}
+        self.specs = [None] * len(protos)
+        self.missing = [len(m) for _d, m in self.plan]
+        self.groups = [None] * len(self.plan)
+        self.launch_order = []
+        self._done = set()
+        self._t0 = None
+
+    def add(self, i: int, spec: FitSpec) -> None:
+        p = self.protos[i]
+        if spec.config != p.config or tuple(spec.target.shape) != tuple(p.target.shape):
+            raise ValueError(f"fit {i}: spec does not match the planned (config, shape)")
+        if self.specs[i] is not None:
+            raise ValueError(f"fit {i} added twice")
+        self.specs[i] = spec
+        gi = self.member_of[i]
+        self.missing[gi] -= 1
+        if self.missing[gi] == 0:
+            self._launch(gi)
+
+    def _launch(self, gi: int) -> None:
+        d, members = self.plan[gi]
+        g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d, True,
+                   self.precision)
+        self.groups[gi] = g
+        if self._t0 is None:
+            self._t0 = torch.cuda.Event(enable_timing=True)
+            self._t0.record(g.stream)
+        g.ev_start.record(g.stream)
+        desc = (_native.NerfhipGroup * 1)(g.desc)
+        st = (ctypes.c_void_p * 1)(g.stream.cuda_stream)
+        _native.check(_native.load().nerfhip_siren_fit(desc, 1, st))
+        g.ev_end.record(g.stream)
+        self.launch_order.append(gi)
+
+    def finished(self, poll_s: float = 0.002):
+        """Yield group indices as their training completes (every group must
+        have been launched, i.e. every fit added)."""
+        if any(m > 0 for m in self.missing):
+            raise ValueError("finished() before every fit was added")
+        left = [gi for gi in self.launch_order if gi not in self._done]
+        while left:
+            ready = [gi for gi in left if self.groups[gi].ev_end.query()]
+            if not ready:
+                time.sleep(poll_s)
+                continue
+            for gi in ready:
+                self._done.add(gi)
+                left.remove(gi)
+                yield gi
+
+    def job_seconds(self) -> float:
+        """First group's start to the last group's end (device clock)."""
+        return max(self._t0.elapsed_time(g.ev_end) for g in self.groups) / 1e3
+
+    def outputs(self, gi: int, job_seconds: float | None = None) -> list:
+        """[(fit index, FitOutput)] of finished group gi.  train_time_seconds:
+        with `job_seconds` (all groups done) the job's wall clock x the fit's
+        FLOP share, as FitJob.outputs; group_seconds is the group's own
+        measured device time either way."""
+        g = self.groups[gi]
+        gs = g.ev_start.elapsed_time(g.ev_end) / 1e3
+        job_f = sum(fit_flops(int(p.target.shape[0]), int(p.target.shape[1]), p.config,
+                              self.epochs) for p in self.protos)
+        outs = g.outputs(self.specs, gs, job_seconds, job_f if job_seconds else None)
+        return list(zip(g.members, outs))
+
+
 def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,
              devices=None, precision: str | None = None) -> list:
     """Train every FitSpec for `epochs` Adam steps; returns FitOutput per spec

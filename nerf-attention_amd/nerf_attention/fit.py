@@ -111,6 +111,56 @@ def _devices(device, gpus) -> list:
     return list(range(gpus))
 
 
+def _stream_ok(plan, epochs, devices, log_every, precision) -> bool:
+    """The streaming path needs one device and one memory wave."""
+    if devices is None or len(devices) != 1 or os.environ.get("NERFHIP_STREAM", "1") == "0":
+        return False
+    need = 0
+    for _n, _l, _h, _kv, cfg, tensor in plan:
+        proto = engine.FitSpec(target=tensor, config=cfg, init=None)
+        need += engine.fit_device_bytes(proto, epochs, log_every, precision)
+    return need <= engine.memory_budget(devices[0])
+
+
+def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precision=None):
+    """train_plan with the host work overlapped (engine.StreamingJob): the
+    models are initialised in plan order (the reference's RNG order) and each
+    group of consecutive same-width fits starts training the moment its last
+    init exists; finished groups are copied back and turned into FitResults
+    while the others still train.  (Checkpoints and stdout wait for the end:
+    each record, which both carry, holds train_time_seconds.)
+    train_time_seconds is the same attribution as train_plan's (the job's
+    wall clock x the fit's FLOP share), fixed up once every group is done;
+    each output's measured `group_seconds` is its group's own device time."""
+    protos = [engine.FitSpec(target=tensor, config=cfg, init=None)
+              for _n, _l, _h, _kv, cfg, tensor in plan]
+    job = engine.StreamingJob(protos, epochs, log_every=log_every, device=device,
+                              precision=precision)
+    models = []
+    for k, (_name, _l, _h, _kv, cfg, tensor) in enumerate(plan):
+        m = SIREN(cfg, out_features=int(tensor.shape[1]))
+        models.append(m)
+        job.add(k, engine.FitSpec(target=tensor, config=cfg, init=m.flat_parameters()))
+    results, outs = [None] * len(plan), [None] * len(plan)
+    dev = torch.device('cuda', device)
+    for gi in job.finished():
+        for k, o in job.outputs(gi):
+            n_rows, d = int(plan[k][5].shape[0]), int(plan[k][5].shape[1])
+            m = models[k].to(dev)
+            m.load_flat_parameters(o.params)
+            m.eval()
+            outs[k] = o
+            results[k] = (_finish(m, plan[k][4], o, n_rows, d), o.probes)
+    job_s = job.job_seconds()
+    flops = [engine.fit_flops(int(p.target.shape[0]), int(p.target.shape[1]), p.config, epochs)
+             for p in protos]
+    tot = sum(flops) or 1.0
+    for k, (res, _p) in enumerate(results):
+        res.train_time_seconds = job_s * flops[k] / tot
+        outs[k].train_time_seconds = res.train_time_seconds
+    return results
+
+
 def train_plan(plan, epochs: int, devices, log_every: int, precision=None):
     """Initialise every model in plan order (the reference's RNG order), then
     train them all on the engine.  Returns [(FitResult, probes)]."""
@@ -170,8 +220,12 @@ def fit_kv_cache(
 
     plan, skipped = sweep_plan(layers, heads, configs, load_layer)
     log_every = max(epochs // 5, 100)
-    results = _host_plan(plan, epochs, log_every) if host else \
-        train_plan(plan, epochs, devices, log_every=log_every, precision=precision)
+    if host:
+        results = _host_plan(plan, epochs, log_every)
+    elif _stream_ok(plan, epochs, devices, log_every, precision):
+        results = train_plan_streaming(plan, epochs, devices[0], log_every, precision)
+    else:
+        results = train_plan(plan, epochs, devices, log_every=log_every, precision=precision)
 
     all_results: list[dict] = []
     count = 0

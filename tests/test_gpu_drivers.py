@@ -169,12 +169,12 @@ def _quick_cache(tmp):
     return kv
 
 
-_NUM = re.compile(r"-?\d+\.\d+")
+_NUM = re.compile(r" *-?\d+\.\d+")   # with its right-aligned padding
 
 
 def _shape(text: str) -> list:
     """stdout line structure: numbers masked, the device name normalised."""
-    return [_NUM.sub("#", l).replace("Device: cuda", "Device: cpu") for l in text.splitlines()]
+    return [_NUM.sub(" #", l).replace("Device: cuda", "Device: cpu") for l in text.splitlines()]
 
 
 def _check_quick_outputs(golden_dir, recs, out_dir):
@@ -314,3 +314,27 @@ def test_fit_device_bytes_covers_group_buffers(gpu):
         need = engine.fit_device_bytes(spec, 20, 5, prec)
         assert need >= held, (cfg.name, need, held)
         assert need <= 1.3 * held + (1 << 20), (cfg.name, need, held)
+
+
+def test_streaming_job_equals_fitjob(gpu):
+    """fit_kv_cache's streaming path (engine.StreamingJob: each group launched
+    the moment its last init exists, results collected as groups finish)
+    trains exactly what a FitJob over the same plan trains: bitwise the same
+    parameters and losses, and the same train_time_seconds attribution rule
+    (the job's wall clock x the fit's FLOP share)."""
+    from nerf_attention import fit as fitmod
+    from nerf_attention.synthetic import kv_cache
+    from nerf_attention.types import CONFIGS_FULL
+    cache = kv_cache([0, 8], 512, 32, 8, 128, heads=range(2))
+    plan, _ = fitmod.sweep_plan([0, 8], 2, CONFIGS_FULL, lambda l: cache[l])
+    torch.manual_seed(0)
+    streamed = fitmod.train_plan_streaming(plan, 40, 0, log_every=20)
+    torch.manual_seed(0)
+    batched = fitmod.train_plan(plan, 40, [0], log_every=20)
+    assert len(streamed) == len(batched) == len(plan) == 56
+    for (a, pa), (b, pb) in zip(streamed, batched):
+        assert torch.equal(a.model.network[-1].weight.cpu(), b.model.network[-1].weight.cpu())
+        assert a.losses == b.losses and pa == pb
+        assert a.final_cosine_mean == b.final_cosine_mean
+    share = [r.train_time_seconds for r, _ in streamed]
+    assert all(t > 0 for t in share)

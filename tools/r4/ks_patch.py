@@ -103,6 +103,37 @@ def sgprs(tok):
     return {int(m.group(1))} if m else set()
 
 
+def vgprs_tok(tok):
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return {f"v{i}" for i in range(int(m.group(1)), int(m.group(2)) + 1)}
+    return {tok} if re.fullmatch(r"v\d+", tok) else set()
+
+
+if patch.startswith("nopvgpr"):
+    # nopvgpr<N>: before every VALU instruction that writes a VGPR read as an
+    # ADDRESS operand (voffset / vaddr) by one of the last 4 vector-memory
+    # instructions, N wait states
+    n = int(patch[len("nopvgpr"):])
+    new, recent, hits = [], [], 0
+    for l in body:
+        t = l.strip()
+        op = t.split()[0] if t and not t.startswith(";") else ""
+        if op.startswith("v_") and not op.startswith(("v_mfma", "v_cmp", "v_readlane", "v_readfirstlane")) and " " in t:
+            dst = vgprs_tok(re.split(r"[,\s]+", t.split(None, 1)[1])[0])
+            if dst and any(dst & r for r in recent):
+                new.append(ins(f"s_nop {n - 1}"))
+                hits += 1
+        if re.match(r"^\.LBB\d+_\d+:", t):
+            recent = []
+        new.append(l)
+        if op.startswith(("buffer_", "global_")):
+            toks = [x for x in re.split(r"[,\s]+", t.split(None, 1)[1]) if x]
+            addr = toks[1] if ("load" in op and " lds" not in t) else toks[0]
+            if op.startswith("global_store") or op.startswith("buffer_store"):
+                addr = toks[0]
+            recent = (recent + [vgprs_tok(addr)])[-4:]
+    print("hits", hits)
 if patch.startswith("nopsmov") or patch == "vm0_after_load_all":
     # nopsmov<N>: before every SALU instruction that writes an SGPR read by one
     # of the last 4 vector-memory instructions (soffset / resource), N wait
@@ -152,7 +183,7 @@ if patch in ("vm0_mfma_all", "nop_accread_all", "vm0_hidden_exit"):
 assert patch in ("none", "vm0_entry", "vm0_mfma", "vm0_load", "vm0_store", "nop_mfma", "nop_load",
                  "bar_entry", "nop_accread", "lgkm0_ds", "vm0_mfma_all", "nop_accread_all",
                  "vm0_hidden_exit") or patch.startswith(("war_pad", "nopsmov")) \
-    or patch == "vm0_after_load_all" or patch.startswith("nopsmov"), patch
+    or patch == "vm0_after_load_all" or patch.startswith(("nopsmov", "nopvgpr")), patch
 src[s:e + 1] = new
 open(out_path, "w").write("\n".join(src))
 print(patch, "final phase lines", fin_start, "..", len(body), "inserted", len(new) - len(body))
