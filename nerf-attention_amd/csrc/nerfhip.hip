@@ -1021,7 +1021,11 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   const float* Wf = P + off_final_w(W, L);
   stage_vec(bias, Wf + W * D, D, tid);
   const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + 4 * g;
-  float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + 4 * g : nullptr;
+  // wave-uniform scalar test (no EXEC write right after the tile stores: a
+  // store still waiting for the memory pipeline can read EXEC late on gfx950,
+  // DESIGN.md §11)
+  const bool has_y = a.y_out != nullptr;
+  float* yo = has_y ? a.y_out + fit * a.y_stride + (int64_t)r * D + 4 * g : nullptr;
   float y[JD][4];
   S8 ys[JD / 2];
   float sq = 0.f;
@@ -1038,7 +1042,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
         }
       },
       [&](int J) {
-        if (yo) st4(yo + 16 * J, y_pend);          // lane holds ŷ[r][16J+4g+q]
+        if (has_y) st4(yo + 16 * J, y_pend);       // lane holds ŷ[r][16J+4g+q]
         if (train) tile_store(SGt, SGb, J, y[J]);
       });
   STAMP(3);
@@ -1163,25 +1167,28 @@ __device__ __forceinline__ void ks_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// A phase's bias vector (n floats, n % 4 == 0) global → LDS.  Diagnostic
-// builds vary how (NERFHIP_EXP_KS_STAGE32: dword stores; _STAGE_ALL: every
-// wave writes the whole vector; _STAGE_BAR: a barrier right after).
-__device__ __forceinline__ void ks_stage(float* dst, const float* src, int n, int tid) {
-#if defined(NERFHIP_EXP_KS_STAGE32)
-  if (4 * tid < n) {
-    const f4 v = ld4(src + 4 * tid);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) dst[4 * tid + q] = v[q];
+// A phase's bias vector (N floats, N compile-time) global → LDS with no
+// change of the EXEC mask: every lane of the waves that take part copies N/64
+// consecutive floats (N >= 256: all four waves; N = 128: waves 0 and 1, a
+// wave-uniform scalar branch).  A divergent `if (4·tid < n)` here narrowed
+// EXEC a few instructions after the phase's weight prefetch had issued; on
+// gfx950 a vector-memory instruction stalled behind a busy memory pipeline
+// can read EXEC after that write, so the masked-off lanes' prefetch never
+// landed (the K-split co-residency fault).
+template <int N>
+__device__ __forceinline__ void ks_stage(float* dst, const float* src, int w, int lane) {
+  static_assert(N % 64 == 0 && N >= 128 && N <= 1024, "bias staging shape");
+  constexpr int WAVES = N >= 256 ? 4 : N / 64, E = N / (64 * WAVES);
+  if (w < WAVES) {                                 // w: an SGPR (readfirstlane)
+    const int i = (w * 64 + lane) * E;
+    if constexpr (E == 4) st4(dst + i, ld4(src + i));
+    else if constexpr (E == 2) {
+      const float2 v = *reinterpret_cast<const float2*>(src + i);
+      *reinterpret_cast<float2*>(dst + i) = v;
+    } else {
+      dst[i] = src[i];
+    }
   }
-#elif defined(NERFHIP_EXP_KS_STAGE_ALL)
-  const int l = tid & 63;
-  for (int i = 4 * l; i < n; i += 256) st4(dst + i, ld4(src + i));
-#else
-  stage_vec(dst, src, n, tid);
-#endif
-#ifdef NERFHIP_EXP_KS_STAGE_BAR
-  ks_barrier();
-#endif
 }
 
 // A-fragment item i of a K-deep phase (tile J = i / NM, this wave's k-slice
@@ -1377,7 +1384,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   ks_prefetch<W>(ring, XS, xm(false, 1), c, g, w);
 
   // ---- layer 0 (K = 1, VALU): this wave's tiles J = 2s + h, s = w + 4m
-  ks_stage(bias, P, 2 * W, tid);
+  ks_stage<2 * W>(bias, P, w, lane);
   __syncthreads();
   const float x = a.pos[r];
   float* SHt = SH + (int64_t)rblk * W * 16 + g * 64 + (c & 3) * 16 + (c >> 2) * 4;
@@ -1403,7 +1410,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 
   // ---- hidden SineLayers 1..L
   for (int i = 1; i <= L; ++i) {
-    ks_stage(bias, P + off_hidden_w(W, i) + W * W, W, tid);
+    ks_stage<W>(bias, P + off_hidden_w(W, i) + W * W, w, lane);
     float* SHi = SH + (int64_t)i * WN + eoff;
     float* SCi = SC + (int64_t)i * WN + coff;
     gemm_ks<W, JW, PD, W>(
@@ -1425,9 +1432,12 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 
   // ---- final nn.Linear(W, D), MSE, dL/dŷ
   KSTAMP(2);
-  ks_stage(bias, P + off_final_w(W, L) + W * D, D, tid);
+  ks_stage<D>(bias, P + off_final_w(W, L) + W * D, w, lane);
   const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + fe;
-  float* yo = a.y_out ? a.y_out + fit * a.y_stride + (int64_t)r * D + fe : nullptr;
+  // no per-lane branches (EXEC writes) in this kernel: whether ŷ is written is
+  // a wave-uniform scalar test of the kernel argument
+  const bool has_y = a.y_out != nullptr;
+  float* yo = has_y ? a.y_out + fit * a.y_stride + (int64_t)r * D + fe : nullptr;
   float* SGe = SG + (int64_t)rblk * D * 16 + fe * 16 + c;
   float sq = 0.f;
   gemm_ks<W, JD, PD, D>(
@@ -1437,7 +1447,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
       [&](int J) { return train_f ? T[16 * J] : 0.f; },
       [&](int J, float acc, float t) {
         const float y = __fadd_rn(acc, bias[16 * J + fe]);
-        if (yo) yo[16 * J] = y;
+        if (has_y) yo[16 * J] = y;
         float gv = 0.f;
         if (train_f) {
           const float diff = y - t;
@@ -1451,7 +1461,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   KSTAMP(3);
   if (!train_f) return;
   sq = wave_sum(sq);
-  if (lane == 0) lsum[w] = sq;
+  lsum[w] = sq;                  // every lane holds the wave's sum
   ys[0] = split_pair(ho[0], ho[1]);
 
   // ---- backward: dZ = (dH ⊙ cos(ωz))·ω, stored for the weight gradients
@@ -1476,7 +1486,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
     bwd(xm(true, i), hs, i - 1, xm(true, i - 1));
   KSTAMP(5);
   // layer 0: cos(ω(x·w0 + b0)) recomputed; dZ0 reduced over the 16 rows at once
-  ks_stage(bias, P, 2 * W, tid);
+  ks_stage<2 * W>(bias, P, w, lane);
   float* PZ = SZ + (int64_t)rblk * 2 * W;
   gemm_ks<W, JW, PD, 0>(
       XS, xm(true, 1), hs, ring, -1, w, c, g, lane, part, outb, no_pre,
@@ -1492,14 +1502,14 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
           sx += __shfl_xor(sx, o, 64);
           s1 += __shfl_xor(s1, o, 64);
         }
-        if (c == 0) {
-          sst(PZ + f, sx);
-          sst(PZ + W + f, s1);
-        }
+        // all 16 lanes of the group hold both sums: lane c = 1 stores Σdz, the
+        // others Σdz·x (identical values to one address) — one store, no EXEC write
+        const bool one = c == 1;
+        sst(one ? PZ + W + f : PZ + f, one ? s1 : sx);
         return 0.f;
       },
       [](int, f4) {});
-  if (tid == 0)
+  if (w == 0)                    // scalar branch; the wave's lanes store one value
     a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] =
         ((lsum[0] + lsum[1]) + lsum[2]) + lsum[3];
   KSTAMP(6);
