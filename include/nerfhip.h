@@ -82,7 +82,9 @@ typedef struct nerfhip_group {
   int32_t D;               /* d_head = out_features                            */
   int32_t N;               /* seq_len                                         */
   int32_t n_fits;
-  int32_t L_max;           /* max hidden_layers over the group (one fit: its own) */
+  int32_t L_max;           /* max hidden_layers over the group.  A one-fit group
+                              MUST set it to that fit's hidden_layers: its kernels
+                              take the depth from L_max, not from fit_layers */
   int32_t epochs;
   int32_t log_every;       /* probe period (siren.py:107); 0 = no probes       */
   int32_t device;          /* HIP device ordinal the buffers and stream live on */
@@ -143,7 +145,8 @@ int nerfhip_siren_fit(const nerfhip_group* groups, int32_t n_groups, void* const
  * the launches of its two step kernels in every 4th epoch (bench.py's
  * roofline leg). */
 typedef struct nerfhip_timing {
-  int32_t launches;        /* out: timed launches per kernel (epochs 3, 7, 11, ...: every 4th, never the cold first) */
+  int32_t launches;        /* out: timed launches per kernel (epochs 3, 7, 11, ...: every 4th, never the cold first);
+                              0 when epochs < 4 — callers must check before dividing */
   int32_t reserved;
   double rows_ms;          /* out: Σ duration of the row-step launches        */
   double params_ms;        /* out: Σ duration of the parameter-step launches  */

@@ -96,6 +96,10 @@ struct KArgs {
   // diagnostic builds only (NERFHIP_STAMPS): per-wave s_memrealtime stamps of
   // the parameter kernel, [blocks][4 waves][8] (NERFHIP_PSTAMPS = device address)
   unsigned long long* pstamps;
+  // dynamic LDS (bytes) the regular row / parameter kernels launch with: an
+  // occupancy knob (a padded row workgroup cannot share its CU with a second
+  // row workgroup, only with a parameter one); 0 = none (make_args)
+  uint32_t rows_dyn_lds, params_dyn_lds;
 };
 template <int W, int D, bool X3> int launch_rows(const KArgs& a, hipStream_t st);
 template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t st);
@@ -2128,7 +2132,8 @@ __global__ void __launch_bounds__(kNormCols * kNormRowGroups) k_normalize(KArgs 
 // (fp32 precision); wsplit ← both split copies (bf16x3 precision).
 __global__ void k_transpose_params(KArgs a) {
   const int fit = blockIdx.y;
-  const int L = a.fit_layers[fit];   // (prologue: not latency-critical)
+  // the same depth the step kernels train (a one-fit group: L_max, nerfhip.h)
+  const int L = fit_layers_of(a, fit);
   const int W = a.W, D = a.D;
   const int64_t nh = (int64_t)L * W * W, total = nh + (int64_t)W * D;
   const float* P = a.params + fit * a.p_stride;
@@ -2322,6 +2327,10 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   a.ws_stride = s.wsplit;
   a.wsplit = static_cast<uint16_t*>(g->wsplit);
   a.rows_ks = rows_ks_for(g, s) ? 1 : 0;
+  // NERFHIP_ROWS_LDS_PAD / NERFHIP_PARAMS_LDS_PAD: dynamic LDS per workgroup
+  // of the regular row / parameter kernels, KB (schedule experiments)
+  if (const char* e = getenv("NERFHIP_ROWS_LDS_PAD")) a.rows_dyn_lds = 1024u * (uint32_t)atoi(e);
+  if (const char* e = getenv("NERFHIP_PARAMS_LDS_PAD")) a.params_dyn_lds = 1024u * (uint32_t)atoi(e);
 #ifdef NERFHIP_STAMPS
   if (const char* e = getenv("NERFHIP_PSTAMPS"))
     a.pstamps = reinterpret_cast<unsigned long long*>(strtoull(e, nullptr, 0));
@@ -2365,8 +2374,8 @@ int launch_rows(const KArgs& a, hipStream_t st) {
   }
   const int grid = grid_for(a.n_fits, a.n_pad / RowsCfg<W>::ROWS);
   if (a.mode == 0)
-    hipLaunchKernelGGL((k_step_rows<W, D, X3, true>), dim3(grid), dim3(RowsCfg<W>::THREADS), 0,
-                       st, a);
+    hipLaunchKernelGGL((k_step_rows<W, D, X3, true>), dim3(grid), dim3(RowsCfg<W>::THREADS),
+                       a.rows_dyn_lds, st, a);
   else
     hipLaunchKernelGGL((k_step_rows<W, D, X3, false>), dim3(grid), dim3(RowsCfg<W>::THREADS), 0,
                        st, a);
@@ -2399,15 +2408,17 @@ int launch_params(const KArgs& a, hipStream_t st) {
     }
   }
   const int grid = grid_for(a.n_fits, ParamsCfg<W, D, X3>::tiles(a.L_max) * a.n_split);
-  if constexpr (X3) {
+  // (the K-split layout epilogue exists only for shapes the K-split row
+  // kernel runs: bf16x3, W >= 128, D = 128 — rows_ks_for)
+  if constexpr (X3 && W >= 128 && D == 128) {
     if (a.rows_ks && a.n_split == 1) {   // fused epilogue writes the K-split layout
       hipLaunchKernelGGL((k_step_params<W, D, X3, false, true>), dim3(grid),
                          dim3(ParamsCfg<W, D, X3>::THREADS), 0, st, a);
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
-  hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS), 0,
-                     st, a);
+  hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS),
+                     a.params_dyn_lds, st, a);
   if (a.n_split > 1) return launch_adam_split<W, D>(a, st);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }

@@ -313,7 +313,15 @@ def _chunks(members: list, cap: int) -> list:
 
 def plan_groups(specs: list, device: int) -> list:
     """[(device, [spec indices])] — fits grouped by (W, d, seq_len), large
-    groups chunked."""
+    groups chunked.
+
+    A group's kernels depend on its size: bf16x3 groups of at most 128
+    regular row workgroups run the K-split row kernel, and groups under 8
+    fits reduce the weight gradient in split-K slices.  Both
+    regroup the same sums, so a fit's result can differ at the rounding level
+    (|Δcos| well under 1e-4) with the chunking or the farm partition that put
+    it in a smaller or larger group; `test_group_chunks_row_variant_rounding`
+    pins that, `test_group_chunks_equal_one_group` the bitwise case."""
     costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
              for s in specs]
     keys = {}

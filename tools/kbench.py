@@ -51,6 +51,8 @@ def main():
         job.launch(timed=True)
         job.wait()
         t = job.timing[0]
+        if t.launches == 0:   # the timed variant times every 4th epoch from epoch 3
+            sys.exit(f"kbench needs --epochs >= 4 (got {args.epochs}): no timed launch")
         rows_ms, par_ms = t.rows_ms / t.launches, t.params_ms / t.launches
         fr, fp = rows_flops(args.seq_len, 128, cf), params_flops(args.seq_len, 128, cf)
         out.append({"rep": rep, "config": args.config, "precision": args.precision, "fits": g.n, "W": g.W,

@@ -19,3 +19,9 @@ for gm in 40 20 80; do for q in 8 16; do
 done; done
 GPU_MAX_HW_QUEUES=8 timeout -k 10 200 python3 tools/r4/sweep_sched.py --epochs 2000 --steps 1 --tag "default-2000" 2>&1 | grep tag >> $out2 || exit 1
 cat $out2
+# (3) forced row/param CU mix: dynamic LDS padding (KB) of the regular row /
+#     parameter kernels (NERFHIP_ROWS_LDS_PAD / NERFHIP_PARAMS_LDS_PAD)
+for pad in "0 0" "8 0" "0 10" "8 2" "6 4"; do set -- $pad
+  NERFHIP_ROWS_LDS_PAD=$1 NERFHIP_PARAMS_LDS_PAD=$2 GPU_MAX_HW_QUEUES=8 timeout -k 10 120 python3 tools/r4/sweep_sched.py --epochs 400 --tag "pad-r$1-p$2" 2>&1 | grep tag >> $out2 || { echo "pad rc=$?"; exit 1; }
+done
+tail -5 $out2
