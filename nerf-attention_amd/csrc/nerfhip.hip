@@ -1146,7 +1146,13 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
 // The k sums are grouped differently from k_step_rows (four partial chains),
 // so a fit's result depends on the row variant at the rounding level.
 // ---------------------------------------------------------------------------
-constexpr unsigned kKsDynLds = 81920;   // bytes of LDS padding per K-split workgroup
+// Dynamic LDS of every K-split workgroup: with its static LDS (≤ 24 592 B
+// at W = 512: partials, finalised tiles, bias) it takes the CU's whole
+// 160 KB, so a K-split workgroup never shares a CU with any workgroup that
+// uses LDS — its own kind or another kernel's (a compile-time
+// forward-only instantiation of this kernel gave wrong blocks when two
+// workgroups shared a CU, and the cause is below the ISA's ordering model).
+constexpr unsigned kKsDynLds = 163840u - 24592u;
 template <int W> struct KsCfg {
   // A-fragment items (S8) in flight per wave.  (W = 256: 10 and 12 items
   // measured 3.5 % and 7 % slower than 6 on one medium fit: not load-latency
@@ -1334,6 +1340,17 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   __shared__ __attribute__((aligned(16))) float bias[2 * W];
   __shared__ float lsum[4];
   int fit, rblk;
+#ifdef NERFHIP_EXP_KS_ALTFIT
+  // diagnostic build: a two-fit group with runs of 256 workgroups alternating
+  // between the fits, so that the two workgroups sharing a CU (b, b + 256)
+  // read different copies of the weights (tools/r3/ks_probe.py KS_FITS=2)
+  if (a.n_fits == 2) {
+    const int b = blockIdx.x;
+    fit = (b >> 8) & 1;
+    rblk = (b & 255) + 256 * (b >> 9);
+    if (rblk >= a.n_pad / 16) return;
+  } else
+#endif
   if (!map_block(blockIdx.x, a.n_fits, a.n_pad / 16, fit, rblk)) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2347,18 +2364,19 @@ int launch_rows(const KArgs& a, hipStream_t st) {
   if constexpr (X3 && W >= 128 && D == 128) {
     if (a.rows_ks) {
       const int grid = grid_for(a.n_fits, a.n_pad / 16);
-      // One K-split workgroup per CU: dynamic LDS padding keeps a second one
-      // off the CU.  A separate forward-only instantiation (MODE = 1, diagnostic
-      // builds only) gave wrong rows in ~1-2 % of the workgroups that shared a
-      // CU with another one (profiles/r03/ks_coresidency.log: the trigger is the
-      // compile-time forward-only FINAL phase, and all four waves' partials of
-      // every final tile are wrong in a bad block); this single runtime-mode
-      // kernel measured correct with and without sharing, and
-      // tests/test_gpu_parity.py::test_rows_ks_coresident pins that.  The
-      // cause was not isolated, so the kernel keeps a CU to itself: up to 64
-      // regular workgroups the grid fits the 256 CUs, up to kKsMaxWorkgroups
-      // (128) it takes two rounds (still faster, rows_ks_for).  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics only) drops the
-      // padding so that two workgroups may share a CU.
+      // One K-split workgroup per CU, alone (kKsDynLds fills the CU's LDS).
+      // A compile-time forward-only instantiation (MODE = 1, diagnostic
+      // builds only) gives wrong 16-row blocks when two workgroups share a
+      // CU; round 4 showed the compiler's vmcnt placement is
+      // correct under the ISA's in-order model and that only waiting for
+      // every load before the next instruction removes the fault, so its
+      // cause lies below that model.  This single runtime-mode kernel has
+      // measured correct with and without sharing in every probe
+      // (tests/test_gpu_parity.py::test_rows_ks_coresident pins it), and it
+      // still never shares a CU: up to 64 regular workgroups its grid fits
+      // the 256 CUs, up to kKsMaxWorkgroups (128) it takes two rounds (still
+      // faster, rows_ks_for).  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics
+      // only) drops the padding so that two workgroups may share a CU.
       const char* e = getenv("NERFHIP_KS_SHARE_CU");
       const unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;
 #ifdef NERFHIP_EXP_KS_MODES

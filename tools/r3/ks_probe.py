@@ -38,7 +38,9 @@ for pad in pads:
         keys, _ = kv_slice(0, 0, seq_len=N, num_layers=1, num_kv_heads=1)
         for rep in range(reps):
             torch.manual_seed(rep)
-            specs = [engine.FitSpec(target=keys, config=cfg, init=SIREN(cfg, 128).flat_parameters())]
+            nf = int(os.environ.get("KS_FITS", "1"))   # 2: two identical fits (ALTFIT builds)
+            init = SIREN(cfg, 128).flat_parameters()
+            specs = [engine.FitSpec(target=keys, config=cfg, init=init) for _ in range(nf)]
             job = engine.FitJob(specs, E, devices=[0], precision="bf16x3", log_every=0)
             g = job.groups[0]
             g.eval_y.fill_(float("nan"))
@@ -49,7 +51,8 @@ for pad in pads:
             m.load_flat_parameters(out.params.cpu())
             with torch.no_grad():
                 y_ref = m.network(torch.linspace(0, 1, N).unsqueeze(1)).double()
-            y = g.eval_y[0, :N].cpu().double()
+            y = torch.cat([g.eval_y[k, :N] for k in range(nf)]).cpu().double()
+            y_ref = torch.cat([y_ref] * nf)
             nan = torch.isnan(y)
             err = (torch.nan_to_num(y, 0.0) - y_ref).abs()
             scale = y_ref.abs().max().item()

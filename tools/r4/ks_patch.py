@@ -14,16 +14,20 @@ import sys
 
 src = open(sys.argv[1]).read().split("\n")
 out_path, patch = sys.argv[2], sys.argv[3]
-name = "_ZN12_GLOBAL__N_114k_step_rows_ksILi256ELi128ELi1EEEvN14nerfhip_detail5KArgsE"
+import os
+name = os.environ.get("KS_SYM", "_ZN12_GLOBAL__N_114k_step_rows_ksILi256ELi128ELi1EEEvN14nerfhip_detail5KArgsE")
 s = next(i for i, l in enumerate(src) if l.startswith(name + ":"))
-e = next(i for i in range(s, len(src)) if src[i].strip() == "s_endpgm" and i > s + 2000)
+e = next(i for i in range(s, len(src)) if src[i].strip().startswith(".Lfunc_end")) - 1
 body = src[s:e + 1]
 # hidden-loop exit: the label after the loop's back-edge branch, then the
 # final phase starts at the first MFMA after it
-loop_exit = next(i for i, l in enumerate(body) if re.match(r"^\.LBB\d+_31:", l.strip()))
-fin_mfma = next(i for i in range(loop_exit, len(body)) if "v_mfma" in body[i])
-# the label just before the first final-phase MFMA
-fin_start = max(i for i in range(loop_exit, fin_mfma) if re.match(r"^\.LBB\d+_\d+:", body[i].strip()))
+try:
+    loop_exit = next(i for i, l in enumerate(body) if re.match(r"^\.LBB\d+_31:", l.strip()))
+    fin_mfma = next(i for i in range(loop_exit, len(body)) if "v_mfma" in body[i])
+    fin_start = max(i for i in range(loop_exit, fin_mfma)
+                    if re.match(r"^\.LBB\d+_\d+:", body[i].strip()))
+except (StopIteration, ValueError):   # another kernel shape: whole-kernel patches only
+    loop_exit = fin_start = len(body) - 1
 
 
 def ins(op):
@@ -142,7 +146,7 @@ if patch.startswith("nopsmov") or patch == "vm0_after_load_all":
     if patch.startswith("nopsmov") and "_" in patch:
         patch, region = patch.split("_", 1)
     n = int(patch[len("nopsmov"):]) if patch.startswith("nopsmov") else 0
-    loop_head = next(i for i, l in enumerate(body) if "Loop Header" in l)
+    loop_head = next((i for i, l in enumerate(body) if "Loop Header" in l), 0)
     lo, hi = {"pro": (0, loop_head - 100), "loop": (loop_head - 100, fin_start),
               "fin": (fin_start, len(body)), None: (0, len(body))}[region]
     new, recent, hits = [], [], 0
