@@ -13,16 +13,19 @@ f32 MFMA ("fp32") or as exact 3-way bf16 splits with six bf16 MFMA products
 per fp32 product and fp32 accumulation ("bf16x3": fp32-class accuracy,
 nerfhip.h nerfhip_precision); everything else is fp32 in both.  Both are held
 to the same per-fit parity bar (cos_delta_vs_ref).  With --also-fp32 (default
-on at N=1) the line also carries one timed fp32 sweep.
+on at N=1) the line also carries the fp32 sweep, timed under the same
+protocol (one warm-up, three timed sweeps).
 
 Also reported (rank 0):
   roofline      the dominant kernel's algorithmic TFLOP/s against the
                 matrix-core peak of its arithmetic (157.3 TFLOP/s f32 MFMA, or
                 2.5 PFLOP/s bf16 dense / 6 products = 416.7 TFLOP/s
                 fp32-equivalent for bf16x3).  `frac` / `achieved` /
-                `avg_launch_ms` are the kernel on its heaviest group timed
-                alone (hipEvents, 40 epochs right after the timed region, the
-                cold first launch excluded); `frac_concurrent` is the same
+                `avg_launch_ms` are the kernel on the engine's heaviest group
+                of its width timed alone (hipEvents on 25 launches of a
+                101-epoch run right after the timed region, the cold first
+                launch excluded; the same leg under rocprofv3 is committed in
+                profiles/r04, tools/r4/iso_prof.sh); `frac_concurrent` is the same
                 kernel's launches inside the timed sweep, where ~7 group
                 streams share the GPU; `job_frac` is the whole sweep's
                 algorithmic rate;
@@ -105,6 +108,12 @@ def host_cpus() -> dict:
     except OSError:
         pass
     threads = min(logical, quota) if quota else logical
+    # one CPU of a quota left to the process's other threads (HIP runtime,
+    # Python): with every quota CPU busy in torch the cgroup throttles the
+    # whole process for part of each 100-ms period, which is where most of the
+    # repeat spread came from (round 3: 11 s throttled in one run)
+    if quota and quota >= 8 and threads == quota:
+        threads -= 1
     return {"affinity_cpus": logical, "cgroup_cpu_quota": quota, "model": model,
             "threads": threads}
 
