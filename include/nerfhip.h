@@ -238,6 +238,25 @@ typedef struct nerfhip_kv_analysis_batch {
 
 int nerfhip_kv_analysis(const nerfhip_kv_analysis_batch* a, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Seeded initialisation replay (host only).  The reference initialises each
+ * SIREN with torch's default CPU generator (siren.py:17-67: nn.Linear's own
+ * reset, then the SIREN re-draw); a sweep draws ~10^8 floats that way, at
+ * ~6 ns each inside torch.  This draws the same sequence at the speed of the
+ * bare generator: mt19937 (state[624], left, next exactly as torch's
+ * CPUGeneratorImpl state holds them) and the float transform of
+ * at::uniform_real_distribution<float> (24 random bits × 2^-24, then
+ * x·(hi−lo)+lo in float).  Segment s consumes counts[s] draws from
+ * U[lo[s], hi[s]) (the bounds are rounded to float as uniform_ does); it
+ * writes them to out + out_off[s], or — out_off[s] < 0 — only advances the
+ * generator (nn.Linear's reset values, which the SIREN overwrites).  The state
+ * is updated in place.  Host memory only; no device, no stream.
+ * ------------------------------------------------------------------------ */
+int nerfhip_rng_uniform_segments(uint32_t* state, int32_t* left, uint32_t* next,
+                                 int32_t n_segments, const int64_t* counts,
+                                 const double* lo, const double* hi,
+                                 const int64_t* out_off, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2378,7 +2378,8 @@ int launch_rows(const KArgs& a, hipStream_t st) {
       // faster, rows_ks_for).  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics
       // only) drops the padding so that two workgroups may share a CU.
       const char* e = getenv("NERFHIP_KS_SHARE_CU");
-      const unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;
+      unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;
+      if (const char* k = getenv("NERFHIP_KS_PAD_KB")) dyn = 1024u * (unsigned)atoi(k);   // diagnostics
 #ifdef NERFHIP_EXP_KS_MODES
       if (a.mode == 0)
         hipLaunchKernelGGL((k_step_rows_ks<W, D, 0>), dim3(grid), dim3(256), dyn, st, a);

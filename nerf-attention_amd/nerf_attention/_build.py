@@ -18,7 +18,8 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 LIB_DIR = PKG / "_lib"
 LIB = LIB_DIR / "libnerfhip.so"
-SOURCES = [CSRC / "nerfhip.hip", CSRC / "nerfhip_svd.hip", CSRC / "nerfhip_analysis.hip"]
+SOURCES = [CSRC / "nerfhip.hip", CSRC / "nerfhip_svd.hip", CSRC / "nerfhip_analysis.hip",
+           CSRC / "nerfhip_rng.cpp"]
 HEADERS = [INCLUDE / "nerfhip.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -95,6 +95,9 @@ SIGNATURES = {
     "nerfhip_group_plan": (c_int32, [POINTER(NerfhipGroup), POINTER(NerfhipPlan)]),
     "nerfhip_svd_rank_metrics": (c_int32, [POINTER(NerfhipSvdBatch), c_void_p]),
     "nerfhip_kv_analysis": (c_int32, [POINTER(NerfhipKvAnalysisBatch), c_void_p]),
+    "nerfhip_rng_uniform_segments": (c_int32, [c_void_p, POINTER(c_int32), POINTER(ctypes.c_uint32),
+                                               c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p]),
 }
 
 _lib = None

@@ -336,9 +336,12 @@ def plan_groups(specs: list, device: int) -> list:
     # keeps every XCD busy.  Measured on the 280-fit sweep: +5 % (160-fit group
     # -> 4 x 40), with GPU_MAX_HW_QUEUES = 8 so the streams get their own queues.
     cap = int(os.environ.get("NERFHIP_GROUP_MAX", str(GROUP_MAX)))
+    # per-width override, e.g. NERFHIP_GROUP_MAX_512=8 (schedule experiments)
+    caps = {w: int(v) for w, v in ((int(k.rsplit("_", 1)[1]), v) for k, v in os.environ.items()
+                                   if k.startswith("NERFHIP_GROUP_MAX_"))}
     parts = []
     for k, m in keys.items():
-        parts += [(k[0], c) for c in _chunks(m, cap)]
+        parts += [(k[0], c) for c in _chunks(m, caps.get(k[1], cap))]
     # heaviest groups first: they are enqueued (and start) first
     return sorted(parts, key=lambda dm: -sum(costs[i] for i in dm[1]))
 

@@ -36,7 +36,7 @@ import numpy as np
 import torch
 
 from . import engine
-from .siren import SIREN, _finish, probe_line
+from .siren import SIREN, _finish, init_flat, probe_line, uninitialised
 from .types import CONFIG_WIDE, CONFIGS_FULL, CONFIGS_QUICK, FitResult, KVMetadata, SIRENConfig
 
 
@@ -124,8 +124,8 @@ def _stream_ok(plan, epochs, devices, log_every, precision) -> bool:
 
 def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precision=None):
     """train_plan with the host work overlapped (engine.StreamingJob): the
-    models are initialised in plan order (the reference's RNG order) and each
-    group of consecutive same-width fits starts training the moment its last
+    inits are drawn in plan order (the reference's RNG order; siren.init_flat,
+    bit-identical to building each SIREN) and each group of consecutive same-width fits starts training the moment its last
     init exists; finished groups are copied back and turned into FitResults
     while the others still train.  (Checkpoints and stdout wait for the end:
     each record, which both carry, holds train_time_seconds.)
@@ -136,17 +136,15 @@ def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precisi
               for _n, _l, _h, _kv, cfg, tensor in plan]
     job = engine.StreamingJob(protos, epochs, log_every=log_every, device=device,
                               precision=precision)
-    models = []
     for k, (_name, _l, _h, _kv, cfg, tensor) in enumerate(plan):
-        m = SIREN(cfg, out_features=int(tensor.shape[1]))
-        models.append(m)
-        job.add(k, engine.FitSpec(target=tensor, config=cfg, init=m.flat_parameters()))
+        job.add(k, engine.FitSpec(target=tensor, config=cfg,
+                                  init=init_flat(cfg, int(tensor.shape[1]))))
     results, outs = [None] * len(plan), [None] * len(plan)
     dev = torch.device('cuda', device)
     for gi in job.finished():
         for k, o in job.outputs(gi):
             n_rows, d = int(plan[k][5].shape[0]), int(plan[k][5].shape[1])
-            m = models[k].to(dev)
+            m = uninitialised(plan[k][4], d, dev)
             m.load_flat_parameters(o.params)
             m.eval()
             outs[k] = o
@@ -162,18 +160,16 @@ def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precisi
 
 
 def train_plan(plan, epochs: int, devices, log_every: int, precision=None):
-    """Initialise every model in plan order (the reference's RNG order), then
-    train them all on the engine.  Returns [(FitResult, probes)]."""
-    models, specs = [], []
-    for _name, _l, _h, _kv, cfg, tensor in plan:
-        m = SIREN(cfg, out_features=int(tensor.shape[1]))
-        models.append(m)
-        specs.append(engine.FitSpec(target=tensor, config=cfg, init=m.flat_parameters()))
+    """Draw every model's init in plan order (the reference's RNG order;
+    siren.init_flat), then train them all on the engine; the returned models
+    are built storage-only (siren.uninitialised) around the trained parameters.  Returns [(FitResult, probes)]."""
+    specs = [engine.FitSpec(target=tensor, config=cfg, init=init_flat(cfg, int(tensor.shape[1])))
+             for _name, _l, _h, _kv, cfg, tensor in plan]
     outs = engine.run_fits(specs, epochs, log_every=log_every, devices=devices,
                            precision=precision)
     results = []
-    for (name, _l, _h, _kv, cfg, tensor), m, o in zip(plan, models, outs):
-        m = m.to(torch.device('cuda', o.device))
+    for (name, _l, _h, _kv, cfg, tensor), o in zip(plan, outs):
+        m = uninitialised(cfg, int(tensor.shape[1]), torch.device('cuda', o.device))
         m.load_flat_parameters(o.params)
         m.eval()
         results.append((_finish(m, cfg, o, int(tensor.shape[0]), int(tensor.shape[1])),

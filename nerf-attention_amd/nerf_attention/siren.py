@@ -19,13 +19,14 @@ host, in eager PyTorch (host_fit.py).
 
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
 import torch
 import torch.nn as nn
 
-from . import engine
+from . import _native, engine
 from .types import FitResult, SIRENConfig
 
 
@@ -127,6 +128,67 @@ class SIREN(nn.Module):
 
     def size_bytes(self) -> int:
         return self.count_parameters() * 4
+
+
+def _init_segments(config: SIRENConfig, out_features: int):
+    """The uniform_ calls SIREN(config, out_features).__init__ makes, in order,
+    as (count, bound, kept): per nn.Linear(in, out) its own reset
+    (kaiming_uniform_ weight, uniform_ bias — overwritten, so only the draw
+    count matters), then the SIREN re-draw of weight and bias in ±bound
+    (siren.py:17-67; bounds as SineLayer / SIREN above compute them)."""
+    w, om = config.hidden_features, config.omega_0
+    linears = [(1, w, 1.0 / 1)]
+    linears += [(w, w, math.sqrt(6.0 / w) / om)] * config.hidden_layers
+    linears += [(w, out_features, math.sqrt(6.0 / w) / om)]
+    segs = []
+    for fan_in, fan_out, bound in linears:
+        segs += [(fan_in * fan_out + fan_out, 0.0, False),
+                 (fan_in * fan_out, bound, True), (fan_out, bound, True)]
+    return segs
+
+
+_STATE = slice(24, 24 + 624 * 8)   # CPUGeneratorImplState: u64 seed, i32 left, i32 seeded,
+_LEFT, _NEXT = slice(8, 12), slice(16, 24)   # u64 next, u64 state[624], normal cache
+
+
+def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
+    """The flat initial parameters `SIREN(config, out_features)` would hold
+    (state_dict order), drawn from — and advancing — torch's default CPU
+    generator exactly as that constructor does, without building the module:
+    nerfhip_rng_uniform_segments replays torch's mt19937 + uniform_ on the
+    host at the bare generator's speed (bit-identical, tests/test_host.py).
+    The sweep's drivers use it to overlap the inits with training."""
+    segs = _init_segments(config, out_features)
+    counts = np.array([c for c, _b, _k in segs], dtype=np.int64)
+    bounds = np.array([b for _c, b, _k in segs], dtype=np.float64)
+    offs, off = np.full(len(segs), -1, dtype=np.int64), 0
+    for i, (c, _b, kept) in enumerate(segs):
+        if kept:
+            offs[i], off = off, off + c
+    flat = torch.empty(off, dtype=torch.float32)
+    raw = torch.get_rng_state().numpy().copy()
+    state = raw[_STATE].view(np.uint64).astype(np.uint32)
+    left = ctypes.c_int32(int(raw[_LEFT].view(np.int32)[0]))
+    nxt = ctypes.c_uint32(int(raw[_NEXT].view(np.uint64)[0]))
+    lo = -bounds
+    _native.check(_native.load().nerfhip_rng_uniform_segments(
+        state.ctypes.data, ctypes.byref(left), ctypes.byref(nxt),
+        len(segs), counts.ctypes.data, lo.ctypes.data, bounds.ctypes.data, offs.ctypes.data,
+        flat.data_ptr()))
+    raw[_STATE].view(np.uint64)[:] = state
+    raw[_LEFT].view(np.int32)[0] = left.value
+    raw[_NEXT].view(np.uint64)[0] = nxt.value
+    torch.set_rng_state(torch.from_numpy(raw))
+    return flat
+
+
+def uninitialised(config: SIRENConfig, out_features: int, device) -> SIREN:
+    """SIREN(config, out_features) on `device` with storage only — built on
+    the meta device, so the constructor draws nothing from the generator —
+    for parameters loaded right after (load_flat_parameters)."""
+    with torch.device('meta'):
+        m = SIREN(config, out_features)
+    return m.to_empty(device=device)
 
 
 def _finish(model: SIREN, config: SIRENConfig, out: engine.FitOutput, seq_len: int,

@@ -12,7 +12,7 @@ import torch
 
 from .engine import FitSpec
 from .fit import select_fits, sweep_plan
-from .siren import SIREN
+from .siren import init_flat
 from .synthetic import kv_cache
 from .types import KVMetadata
 
@@ -39,8 +39,6 @@ def sweep_280(seq_len: int = 2048, seed: int | None = 0, quick: bool = False,
     plan, _ = sweep_plan(layers, heads, configs, load)
     if seed is not None:
         torch.manual_seed(seed)
-    specs = []
-    for _name, _l, _h, _kv, cfg, tensor in plan:
-        m = SIREN(cfg, out_features=int(tensor.shape[1]))
-        specs.append(FitSpec(target=tensor, config=cfg, init=m.flat_parameters()))
+    specs = [FitSpec(target=tensor, config=cfg, init=init_flat(cfg, int(tensor.shape[1])))
+             for _name, _l, _h, _kv, cfg, tensor in plan]
     return plan, specs

@@ -6,6 +6,7 @@ import re
 import subprocess
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 from nerf_attention import _build, _native
@@ -127,3 +128,52 @@ def test_group_plan(lib):
     assert p.rows_workgroups == 5 * 512 // 16
     assert _plan(lib, W=100, D=128, N=64, n_fits=1, L_max=1, epochs=1)[0] == -1
     assert lib.nerfhip_group_plan(None, None) == -5
+
+
+def _mt_seed(seed):
+    """std::mt19937's seeding recurrence (torch's init_with_uint32)."""
+    s = np.zeros(624, dtype=np.uint32)
+    s[0] = seed
+    for j in range(1, 624):
+        p = int(s[j - 1])
+        s[j] = (1812433253 * (p ^ (p >> 30)) + j) & 0xFFFFFFFF
+    return s
+
+
+def test_rng_known_answers(lib):
+    """nerfhip_rng_uniform_segments on U[0, 1): draw k is (y_k & 2^24-1)/2^24
+    for the tempered mt19937 output y_k.  Known answers of the standard
+    generator, seed 5489: y_1 = 3499211612, y_10000 = 4123659995 (the C++
+    standard's check value); discarded segments advance the same words."""
+    st, left, nxt = _mt_seed(5489), ctypes.c_int32(1), ctypes.c_uint32(0)
+    out = np.zeros(3, dtype=np.float32)
+    counts = np.array([1, 9998, 1, 1], dtype=np.int64)
+    lo, hi = np.zeros(4), np.ones(4)
+    off = np.array([0, -1, 1, 2], dtype=np.int64)
+    assert lib.nerfhip_rng_uniform_segments(
+        st.ctypes.data, ctypes.byref(left), ctypes.byref(nxt), 4, counts.ctypes.data,
+        lo.ctypes.data, hi.ctypes.data, off.ctypes.data, out.ctypes.data) == 0
+    assert out[0] == np.float32((3499211612 & 0xFFFFFF) / 2.0 ** 24)
+    assert out[1] == np.float32((4123659995 & 0xFFFFFF) / 2.0 ** 24)
+    assert (left.value, nxt.value) == (624 - (10001 - 624 * 16) + 1, 10001 - 624 * 16)
+
+
+def test_rng_rejects_without_moving_state(lib):
+    st, left, nxt = _mt_seed(1), ctypes.c_int32(1), ctypes.c_uint32(0)
+    keep = st.copy()
+    counts = np.array([5, -1], dtype=np.int64)
+    lo, hi, off = np.zeros(2), np.ones(2), np.array([-1, -1], dtype=np.int64)
+    args = (counts.ctypes.data, lo.ctypes.data, hi.ctypes.data, off.ctypes.data)
+    assert lib.nerfhip_rng_uniform_segments(st.ctypes.data, ctypes.byref(left),
+                                            ctypes.byref(nxt), 2, *args, None) == -4
+    assert np.array_equal(st, keep) and (left.value, nxt.value) == (1, 0)
+    off[0] = 0                                               # kept segment, no output buffer
+    counts[1] = 1
+    assert lib.nerfhip_rng_uniform_segments(st.ctypes.data, ctypes.byref(left),
+                                            ctypes.byref(nxt), 2, *args, None) == -5
+    assert lib.nerfhip_rng_uniform_segments(None, ctypes.byref(left), ctypes.byref(nxt),
+                                            0, None, None, None, None, None) == -5
+    left.value = 0                                           # not a valid generator state
+    assert lib.nerfhip_rng_uniform_segments(st.ctypes.data, ctypes.byref(left),
+                                            ctypes.byref(nxt), 0, None, None, None, None,
+                                            None) == -4

@@ -223,3 +223,43 @@ def test_param_tiles_matches_kernel_grid():
     assert engine.param_tiles(64, 128, 1) == 4        # tiny
     assert 5 * engine.param_tiles(512, 128, 2) >= engine.SPLIT_MIN_TILES    # 8-rank large group: fused
     assert engine.param_tiles(256, 128, 2) < engine.SPLIT_MIN_TILES         # config 2: split-K
+
+
+# --- native init replay (siren.init_flat / nerfhip_rng_uniform_segments) ---
+
+@pytest.mark.parametrize("seed", [0, 1, 12345])
+@pytest.mark.parametrize("w,layers,d", [(64, 1, 128), (128, 2, 64), (256, 3, 128), (512, 2, 64)])
+def test_init_flat_equals_siren_constructor(seed, w, layers, d):
+    """Same bits as SIREN(cfg, d).flat_parameters(), and the generator left
+    where the constructor leaves it (a torch draw before and after agrees)."""
+    from nerf_attention.siren import init_flat
+    cfg = SIRENConfig(w, layers, 30.0, "t")
+    torch.manual_seed(seed)
+    torch.rand(seed % 97)
+    a, a_next = init_flat(cfg, d), torch.rand(7)
+    torch.manual_seed(seed)
+    torch.rand(seed % 97)
+    b, b_next = SIREN(cfg, d).flat_parameters(), torch.rand(7)
+    assert torch.equal(a, b)
+    assert torch.equal(a_next, b_next)
+
+
+def test_init_flat_sweep_order(golden_dir):
+    """The 280 sweep inits drawn natively == the reference's sequential run."""
+    from nerf_attention.siren import init_flat
+    ref = json.loads((golden_dir / "sweep_init_order.json").read_text())
+    cfg = {c.name: c for c in CONFIGS_FULL}
+    torch.manual_seed(0)
+    for name, h in ref:
+        assert sha(init_flat(cfg[name.split("_")[-1]], 128).numpy()) == h, name
+
+
+def test_uninitialised_draws_nothing():
+    from nerf_attention.siren import uninitialised
+    cfg = {c.name: c for c in CONFIGS_FULL}["medium"]
+    torch.manual_seed(3)
+    before = torch.get_rng_state()
+    m = uninitialised(cfg, 128, "cpu")
+    assert torch.equal(before, torch.get_rng_state())
+    assert list(m.state_dict()) == list(SIREN(cfg, 128).state_dict())
+    assert m.count_parameters() == cfg.num_parameters(128)
