@@ -25,6 +25,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import threading
 import time
 from dataclasses import dataclass, field
 
@@ -162,7 +163,21 @@ class _Group:
         self.n, self.n_pad = n, n_pad
         dev = torch.device("cuda", device)
         f32 = dict(dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            # (high priority for the light W=64/128 groups: +3 % on one box, ±0 on
+            # another — box-to-box spread is ±2 %; not adopted)
+            self.stream = torch.cuda.Stream(device=dev)
+            self.stream.wait_stream(torch.cuda.current_stream(dev))  # callers' prior work
+            self.ev_start = torch.cuda.Event(enable_timing=True)
+            self.ev_end = torch.cuda.Event(enable_timing=True)
+        # uploads and allocations on the group's own stream: a copy on the
+        # default stream would queue behind whatever other groups keep the
+        # device busy with (StreamingJob builds groups while others train)
+        with torch.cuda.stream(self.stream):
+            self._build(members, specs, lr, dev, f32, cfgs, s, split, precision)
 
+    def _build(self, members, specs, lr, dev, f32, cfgs, s, split, precision):
+        n, n_pad, epochs = self.n, self.n_pad, self.epochs
         # packing (the reference's H2D copies, siren.py:82-89): on the host and
         # one copy per buffer when the inputs are host tensors, directly on the
         # device when the caller already holds them there (torch.ops.nerfhip)
@@ -221,7 +236,7 @@ class _Group:
         ptr = lambda t: None if t is None else t.data_ptr()
         self.desc = _native.NerfhipGroup(
             W=self.W, D=self.D, N=self.N, n_fits=n, L_max=self.L_max, epochs=epochs,
-            log_every=self.log_every, device=device, precision=_native.PRECISIONS[precision],
+            log_every=self.log_every, device=self.device, precision=_native.PRECISIONS[precision],
             fit_layers=ptr(self.layers), fit_omega=ptr(self.omega), positions=ptr(self.pos),
             target=ptr(self.target), target_norm=ptr(self.target_norm), mean=ptr(self.mean),
             std=ptr(self.std), params=ptr(self.params), params_t=ptr(self.params_t),
@@ -231,13 +246,6 @@ class _Group:
             row_sq=ptr(self.row_sq), probe_row_cos=ptr(self.probe_row_cos),
             probe_row_sq=ptr(self.probe_row_sq), grad_partial=ptr(self.grad_partial),
             wsplit=ptr(self.wsplit))
-        with torch.cuda.device(dev):
-            # (high priority for the light W=64/128 groups: +3 % on one box, ±0 on
-            # another — box-to-box spread is ±2 %; not adopted)
-            self.stream = torch.cuda.Stream(device=dev)
-            self.stream.wait_stream(torch.cuda.current_stream(dev))  # H2D copies above
-            self.ev_start = torch.cuda.Event(enable_timing=True)
-            self.ev_end = torch.cuda.Event(enable_timing=True)
 
     def plan(self) -> dict:
         """How the engine runs this group's epoch (nerfhip_group_plan): the row
@@ -428,8 +436,10 @@ class StreamingJob:
     (config, seq_len, d_head) — `plan_groups` needs nothing else — and
     `add(i, spec)` hands over fit i's target and init: the moment the last
     member of a group (a chunk of consecutive reference-order fits of one
-    width) arrives, that group's buffers are packed and its whole training is
-    enqueued on its own stream, while the host goes on drawing the next inits.
+    width) arrives, a launcher thread of that group packs and uploads its
+    buffers and enqueues its whole training on its own stream (that call
+    blocks on the stream's queue depth for most of the run), while the
+    caller goes on drawing the next inits.
     `finished()` then yields groups in the order they complete, so results,
     checkpoints and progress lines can be produced while the rest still
     trains.  Results are bitwise those of a FitJob over the same groups: the
@@ -450,7 +460,7 @@ class StreamingJob:
         self.groups = [None] * len(self.plan)
         self.launch_order = []
         self._done = set()
-        self._t0 = None
+        self._threads, self._errors = {}, {}
 
     def add(self, i: int, spec: FitSpec) -> None:
         p = self.protos[i]
@@ -465,28 +475,49 @@ class StreamingJob:
             self._launch(gi)
 
     def _launch(self, gi: int) -> None:
-        d, members = self.plan[gi]
-        g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d, True,
-                   self.precision)
-        self.groups[gi] = g
-        if self._t0 is None:
-            self._t0 = torch.cuda.Event(enable_timing=True)
-            self._t0.record(g.stream)
-        g.ev_start.record(g.stream)
-        desc = (_native.NerfhipGroup * 1)(g.desc)
-        st = (ctypes.c_void_p * 1)(g.stream.cuda_stream)
-        _native.check(_native.load().nerfhip_siren_fit(desc, 1, st))
-        g.ev_end.record(g.stream)
+        # Enqueueing a group's whole training (≈ 2 launches per epoch) blocks
+        # once its stream's hardware queue is full, i.e. for most of the
+        # group's run; from the caller's thread that would hold back every
+        # later group's launch (and the next inits).  So each group is packed,
+        # uploaded (on its own stream) and enqueued by a thread of its own;
+        # the C call releases the GIL.
+        t = threading.Thread(target=self._run, args=(gi,), name=f"nerfhip-group-{gi}",
+                             daemon=True)
+        self._threads[gi] = t
         self.launch_order.append(gi)
+        t.start()
+
+    def _run(self, gi: int) -> None:
+        try:
+            d, members = self.plan[gi]
+            g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d, True,
+                       self.precision)
+            self.groups[gi] = g
+            g.ev_start.record(g.stream)
+            desc = (_native.NerfhipGroup * 1)(g.desc)
+            st = (ctypes.c_void_p * 1)(g.stream.cuda_stream)
+            _native.check(_native.load().nerfhip_siren_fit(desc, 1, st))
+            g.ev_end.record(g.stream)
+        except BaseException as e:          # re-raised by finished()
+            self._errors[gi] = e
 
     def finished(self, poll_s: float = 0.002):
         """Yield group indices as their training completes (every group must
-        have been launched, i.e. every fit added)."""
+        have been launched, i.e. every fit added).  A group counts once its
+        launcher thread is done and its end event has completed."""
         if any(m > 0 for m in self.missing):
             raise ValueError("finished() before every fit was added")
         left = [gi for gi in self.launch_order if gi not in self._done]
         while left:
-            ready = [gi for gi in left if self.groups[gi].ev_end.query()]
+            ready = []
+            for gi in left:
+                if self._threads[gi].is_alive():
+                    continue
+                if gi in self._errors:
+                    self._join_all()
+                    raise self._errors[gi]
+                if self.groups[gi].ev_end.query():
+                    ready.append(gi)
             if not ready:
                 time.sleep(poll_s)
                 continue
@@ -495,9 +526,19 @@ class StreamingJob:
                 left.remove(gi)
                 yield gi
 
+    def _join_all(self) -> None:
+        for t in self._threads.values():
+            t.join()
+
     def job_seconds(self) -> float:
-        """First group's start to the last group's end (device clock)."""
-        return max(self._t0.elapsed_time(g.ev_end) for g in self.groups) / 1e3
+        """Earliest group start to the last group's end (device clock)."""
+        self._join_all()
+        starts = [g.ev_start for g in self.groups]
+        first = starts[0]
+        for ev in starts[1:]:
+            if ev.elapsed_time(first) > 0:        # ev recorded before `first`
+                first = ev
+        return max(first.elapsed_time(g.ev_end) for g in self.groups) / 1e3
 
     def outputs(self, gi: int, job_seconds: float | None = None) -> list:
         """[(fit index, FitOutput)] of finished group gi.  train_time_seconds:
