@@ -49,9 +49,12 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "nerf-attention_amd"))
 
 # one hardware queue per width-group stream (the engine runs ~7 streams per
-# GPU; HIP's default of 4 queues makes some of them share a queue, in order).
-# Must be set before the HIP runtime initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# GPU; HIP's default of 4 queues makes some of them share a queue, in order:
+# the 2000-epoch sweep measured 27.0 fits/s with 4, 27.7 with 8 on one box,
+# profiles/r04/queues_ab.log).  The GPU boxes export HIP's default (4), so it
+# is raised, not defaulted.  Must be set before the HIP runtime initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np
 import torch

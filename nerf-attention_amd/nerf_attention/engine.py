@@ -116,6 +116,10 @@ SPLIT_MAX_FITS = 8   # groups below this size split the gradient reduction (grad
 # 168 -> 185 fits/s), 5 small fits (20 tiles) 3.5x slower fused
 # (profiles/r02/split_probe.log)
 SPLIT_MIN_TILES = 128
+# FitJob.launch: one launcher thread per group (each group's enqueue blocks on
+# its own stream's queue depth only) instead of one thread interleaving the
+# groups epoch by epoch
+LAUNCH_THREADS = os.environ.get("NERFHIP_LAUNCH_THREADS", "0") == "1"
 
 
 def param_tiles(W: int, D: int, L: int) -> int:
@@ -382,6 +386,7 @@ class FitJob:
         self._streams = (ctypes.c_void_p * G)(*[g.stream.cuda_stream for g in self.groups])
         self.fresh = True
         self.timing = None
+        self._threads, self._errors = [], {}
 
     def reset(self) -> None:
         for g in self.groups:
@@ -392,10 +397,20 @@ class FitJob:
     def launch(self, timed: bool = False) -> None:
         """Enqueue every group.  timed=True brackets every step-kernel launch
         with hipEvents (self.timing[i] per group; synchronises the groups)."""
+        for t in self._threads:                      # a previous threaded launch
+            t.join()
         if not self.fresh:
             self.reset()
         self.fresh = False
         G = len(self.groups)
+        if not timed and G > 1 and LAUNCH_THREADS:
+            self.timing = None
+            self._threads = [threading.Thread(target=self._launch_one, args=(i,), daemon=True,
+                                              name=f"nerfhip-group-{i}") for i in range(G)]
+            self._errors = {}
+            for t in self._threads:
+                t.start()
+            return
         for g in self.groups:
             g.ev_start.record(g.stream)
         if not timed:
@@ -408,7 +423,23 @@ class FitJob:
         for g in self.groups:
             g.ev_end.record(g.stream)
 
+    def _launch_one(self, i: int) -> None:
+        g = self.groups[i]
+        try:
+            g.ev_start.record(g.stream)
+            desc = (_native.NerfhipGroup * 1)(g.desc)
+            st = (ctypes.c_void_p * 1)(g.stream.cuda_stream)
+            _native.check(_native.load().nerfhip_siren_fit(desc, 1, st))
+            g.ev_end.record(g.stream)
+        except BaseException as e:          # re-raised by wait()
+            self._errors[i] = e
+
     def wait(self) -> None:
+        for t in self._threads:
+            t.join()
+        self._threads = []
+        if self._errors:
+            raise next(iter(self._errors.values()))
         for g in self.groups:
             g.ev_end.synchronize()
 

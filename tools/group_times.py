@@ -6,7 +6,8 @@ import os
 import sys
 from pathlib import Path
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8 and "SWEEP_KEEP_QUEUES" not in os.environ:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "nerf-attention_amd"))
 import torch  # noqa: E402
