@@ -338,3 +338,32 @@ def test_streaming_job_equals_fitjob(gpu):
         assert a.final_cosine_mean == b.final_cosine_mean
     share = [r.train_time_seconds for r, _ in streamed]
     assert all(t > 0 for t in share)
+
+
+@pytest.mark.gpu
+def test_fitjob_threaded_launch_is_bitwise_equal(gpu, monkeypatch):
+    """FitJob.launch with one launcher thread per group (NERFHIP_LAUNCH_THREADS)
+    trains exactly what the single interleaving thread trains, launch after
+    launch (reset + relaunch, as bench.py's steps do)."""
+    from nerf_attention import engine
+    from nerf_attention.siren import init_flat
+    from nerf_attention.synthetic import kv_cache
+    from nerf_attention.types import CONFIGS_FULL
+    cache = kv_cache([0], 512, 32, 8, 128, heads=range(2))
+    torch.manual_seed(0)
+    specs = [engine.FitSpec(target=cache[0][kv][h], config=c, init=init_flat(c, 128))
+             for h in range(2) for kv in ("keys", "values") for c in CONFIGS_FULL]
+    outs = {}
+    for threads in (False, True):
+        monkeypatch.setattr(engine, "LAUNCH_THREADS", threads)
+        job = engine.FitJob(specs, 30, devices=[0], precision="bf16x3")
+        assert len(job.groups) > 1
+        runs = []
+        for _ in range(2):
+            job.launch()
+            job.wait()
+            runs.append([o.params.cpu() for o in job.outputs()])
+        assert all(torch.equal(a, b) for a, b in zip(*runs))
+        outs[threads] = runs[0]
+        del job
+    assert all(torch.equal(a, b) for a, b in zip(outs[False], outs[True]))
