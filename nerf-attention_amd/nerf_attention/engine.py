@@ -148,7 +148,7 @@ class _Group:
     """Device buffers + descriptor of one (device, W, d, seq_len) group."""
 
     def __init__(self, members, specs, epochs, lr, log_every, device, split=True,
-                 precision="fp32"):
+                 precision="fp32", priority=0):
         self.members = members
         self.precision = precision
         cfgs = [specs[i].config for i in members]
@@ -170,7 +170,7 @@ class _Group:
         with torch.cuda.device(dev):
             # (high priority for the light W=64/128 groups: +3 % on one box, ±0 on
             # another — box-to-box spread is ±2 %; not adopted)
-            self.stream = torch.cuda.Stream(device=dev)
+            self.stream = torch.cuda.Stream(device=dev, priority=priority)
             self.stream.wait_stream(torch.cuda.current_stream(dev))  # callers' prior work
             self.ev_start = torch.cuda.Event(enable_timing=True)
             self.ev_end = torch.cuda.Event(enable_timing=True)
@@ -379,8 +379,12 @@ class FitJob:
         self.specs = specs
         self.epochs = epochs
         self.plan = plan_groups(specs, self.device)
-        self.groups = [_Group(m, specs, epochs, lr, log_every, d, split, self.precision)
-                       for d, m in self.plan]
+        # (diagnostic: NERFHIP_PRIO_HEAVY=1 gives the heaviest group, the
+        # sweep's critical path, a high-priority stream)
+        heavy = os.environ.get("NERFHIP_PRIO_HEAVY", "0") == "1"
+        self.groups = [_Group(m, specs, epochs, lr, log_every, d, split, self.precision,
+                              priority=-1 if (heavy and k == 0) else 0)
+                       for k, (d, m) in enumerate(self.plan)]
         G = len(self.groups)
         self._descs = (_native.NerfhipGroup * G)(*[g.desc for g in self.groups])
         self._streams = (ctypes.c_void_p * G)(*[g.stream.cuda_stream for g in self.groups])
