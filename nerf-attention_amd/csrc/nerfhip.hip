@@ -304,10 +304,16 @@ __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32
   const uint32_t u = __float_as_uint(x);
   const float r1 = x - __uint_as_float(u & 0xffff0000u);
   const uint32_t u1 = __float_as_uint(r1);
+#ifdef NERFHIP_EXP_X2PROXY
+  h = u;
+  m = u1;
+  l = u1;
+#else
   const float r2 = r1 - __uint_as_float(u1 & 0xffff0000u);
   h = u;
   m = u1;
   l = __float_as_uint(r2);   // ≤ 8 significant bits: its top half is exact
+#endif
 }
 // low half ← bf16 of a, high half ← bf16 of b (the top 16 bits of each): one
 // v_perm_b32 (bytes 2,3 of a then bytes 2,3 of b; {S0,S1} = {b,a}) instead of
@@ -343,6 +349,22 @@ __device__ __forceinline__ f16v mfma32b(u4 a, u4 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                  __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
 }
+// NERFHIP_EXP_X2PROXY (diagnostic timing build, WRONG numerics): the cost of
+// a two-plane operand split with three products (hi·hi', hi·lo', lo·hi', as
+// an fp16 hi/lo split with power-of-two scaling would need): the m plane
+// stands in for lo, the l plane is neither split, staged, read nor multiplied.
+#ifdef NERFHIP_EXP_X2PROXY
+__device__ __forceinline__ void mfma16x3(const S8& a, const S8& b, f4& hi, f4& lo) {
+  lo = mfma16b(a.h, b.m, lo);
+  lo = mfma16b(a.m, b.h, lo);
+  hi = mfma16b(a.h, b.h, hi);
+}
+__device__ __forceinline__ void mfma32x3(const S8& a, const S8& b, f16v& hi, f16v& lo) {
+  lo = mfma32b(a.h, b.m, lo);
+  lo = mfma32b(a.m, b.h, lo);
+  hi = mfma32b(a.h, b.h, hi);
+}
+#else
 __device__ __forceinline__ void mfma16x3(const S8& a, const S8& b, f4& hi, f4& lo) {
   lo = mfma16b(a.h, b.l, lo);
   lo = mfma16b(a.l, b.h, lo);
@@ -359,6 +381,7 @@ __device__ __forceinline__ void mfma32x3(const S8& a, const S8& b, f16v& hi, f16
   lo = mfma32b(a.m, b.h, lo);
   hi = mfma32b(a.h, b.h, hi);
 }
+#endif
 
 // Split-plane layout of a weight matrix M[R][K] (R % 16 == 0, K % 32 == 0):
 // [R/16][K/KC][3 planes][16 rows][KC] bf16, KC = min(K, 256), so a 16-row ×
@@ -643,7 +666,11 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
   constexpr int SWM = (SR < 16 ? SR : 16) - 1;              // swizzle mask
   constexpr int CH = 3 * 16 * KC;                           // bf16 per ring buffer
   constexpr int PLB = 32 * KC;                              // bytes per plane
+#ifdef NERFHIP_EXP_X2PROXY
+  constexpr int SL = 2 * 16 * SR, NPT = (SL + NTH - 1) / NTH;   // planes 0, 1 only
+#else
   constexpr int SL = 3 * 16 * SR, NPT = (SL + NTH - 1) / NTH;   // slots per sub-chunk
+#endif
   constexpr int NDMA = SL / NTH;                                // DMAs every wave issues
   constexpr int QSTEP = (KT - 1) / 4 > 0 ? (KT - 1) / 4 : 1;
   typedef __attribute__((address_space(3))) void lds_void;
@@ -693,8 +720,12 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
     S8 r;
     r.h = ds_read16<OFF>(abase[kt]);
     r.m = ds_read16<OFF + PLB>(abase[kt]);
+#ifdef NERFHIP_EXP_X2PROXY
+    r.l = r.m;
+#else
     if constexpr (OFF + 2 * PLB < 65536) r.l = ds_read16<OFF + 2 * PLB>(abase[kt]);
     else r.l = ds_read16<OFF + PLB>(abase[kt] + PLB);
+#endif
     return r;
   };
   auto lgkm_wait = [](S8& r) {
@@ -1802,7 +1833,11 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
         const u2 vl = {pk_top(sl[0], sl[1]), pk_top(sl[2], sl[3])};
         *reinterpret_cast<u2*>(d) = vh;
         *reinterpret_cast<u2*>(d + PLX) = vm;
+#ifdef NERFHIP_EXP_X2PROXY
+        (void)vl;
+#else
         *reinterpret_cast<u2*>(d + 2 * PLX) = vl;
+#endif
         if (m < NPA && i < NA4 && count) bpart[m] += (v[0] + v[1]) + (v[2] + v[3]);
       }
     }
@@ -1825,7 +1860,11 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     S8 r;
     r.h = *reinterpret_cast<const u4*>(q);
     r.m = *reinterpret_cast<const u4*>(q + PLX);
+#ifdef NERFHIP_EXP_X2PROXY
+    r.l = r.m;
+#else
     r.l = *reinterpret_cast<const u4*>(q + 2 * PLX);
+#endif
     return r;
   };
 
