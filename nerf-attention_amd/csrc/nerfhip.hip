@@ -300,11 +300,16 @@ struct S8 {            // one lane's 8 k-values of an MFMA operand, three planes
   u4 h, m, l;
 };
 
+#ifndef NERFHIP_EXP_X2PROXY   // diagnostic timing builds only, see mfma16x3
+#define NERFHIP_X2P(bit) 0
+#else
+#define NERFHIP_X2P(bit) ((NERFHIP_EXP_X2PROXY) & (bit))
+#endif
 __device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
   const uint32_t u = __float_as_uint(x);
   const float r1 = x - __uint_as_float(u & 0xffff0000u);
   const uint32_t u1 = __float_as_uint(r1);
-#ifdef NERFHIP_EXP_X2PROXY
+#if NERFHIP_X2P(8)
   h = u;
   m = u1;
   l = u1;
@@ -353,7 +358,10 @@ __device__ __forceinline__ f16v mfma32b(u4 a, u4 b, f16v c) {
 // a two-plane operand split with three products (hi·hi', hi·lo', lo·hi', as
 // an fp16 hi/lo split with power-of-two scaling would need): the m plane
 // stands in for lo, the l plane is neither split, staged, read nor multiplied.
-#ifdef NERFHIP_EXP_X2PROXY
+// Bit flags: 1 three products, 2 row-kernel weight DMA of two planes, 4 its
+// A-fragment LDS reads of two planes, 8 no l in split3, 16 the parameter
+// kernel's staging and reads of two planes (31 = all, 30 = data movement only).
+#if NERFHIP_X2P(1)
 __device__ __forceinline__ void mfma16x3(const S8& a, const S8& b, f4& hi, f4& lo) {
   lo = mfma16b(a.h, b.m, lo);
   lo = mfma16b(a.m, b.h, lo);
@@ -666,7 +674,7 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
   constexpr int SWM = (SR < 16 ? SR : 16) - 1;              // swizzle mask
   constexpr int CH = 3 * 16 * KC;                           // bf16 per ring buffer
   constexpr int PLB = 32 * KC;                              // bytes per plane
-#ifdef NERFHIP_EXP_X2PROXY
+#if NERFHIP_X2P(2)
   constexpr int SL = 2 * 16 * SR, NPT = (SL + NTH - 1) / NTH;   // planes 0, 1 only
 #else
   constexpr int SL = 3 * 16 * SR, NPT = (SL + NTH - 1) / NTH;   // slots per sub-chunk
@@ -720,7 +728,7 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
     S8 r;
     r.h = ds_read16<OFF>(abase[kt]);
     r.m = ds_read16<OFF + PLB>(abase[kt]);
-#ifdef NERFHIP_EXP_X2PROXY
+#if NERFHIP_X2P(4)
     r.l = r.m;
 #else
     if constexpr (OFF + 2 * PLB < 65536) r.l = ds_read16<OFF + 2 * PLB>(abase[kt]);
@@ -1833,7 +1841,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
         const u2 vl = {pk_top(sl[0], sl[1]), pk_top(sl[2], sl[3])};
         *reinterpret_cast<u2*>(d) = vh;
         *reinterpret_cast<u2*>(d + PLX) = vm;
-#ifdef NERFHIP_EXP_X2PROXY
+#if NERFHIP_X2P(16)
         (void)vl;
 #else
         *reinterpret_cast<u2*>(d + 2 * PLX) = vl;
@@ -1860,7 +1868,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     S8 r;
     r.h = *reinterpret_cast<const u4*>(q);
     r.m = *reinterpret_cast<const u4*>(q + PLX);
-#ifdef NERFHIP_EXP_X2PROXY
+#if NERFHIP_X2P(16)
     r.l = r.m;
 #else
     r.l = *reinterpret_cast<const u4*>(q + 2 * PLX);
