@@ -207,3 +207,24 @@ def test_bench_cpu_baseline_times_host_path():
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["bad"] == [] and out["kind"] == "port" and "host_fit" in out["port"]
     assert out["value"] > 0 and out["archs"] == 7
+
+
+@pytest.mark.parametrize("given,want", [(None, "8"), ("4", "8"), ("16", "16")])
+def test_bench_raises_hw_queues(given, want):
+    """bench.py gives every group stream its own hardware queue: it raises
+    GPU_MAX_HW_QUEUES to 8 when unset or lower (the GPU boxes export HIP's
+    default of 4) and keeps a higher setting."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    if given is not None:
+        env["GPU_MAX_HW_QUEUES"] = given
+    code = (f"import os, sys; sys.path.insert(0, {str(root)!r}); import bench; "
+            "print(os.environ['GPU_MAX_HW_QUEUES'])")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       timeout=300, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == want
