@@ -148,7 +148,8 @@ def _init_segments(config: SIRENConfig, out_features: int):
 
 
 _STATE = slice(24, 24 + 624 * 8)   # CPUGeneratorImplState: u64 seed, i32 left, i32 seeded,
-_LEFT, _NEXT = slice(8, 12), slice(16, 24)   # u64 next, u64 state[624], normal cache
+_LEFT, _SEEDED, _NEXT = slice(8, 12), slice(12, 16), slice(16, 24)   # u64 next, u64 state[624],
+_STATE_BYTES = 5056                                                    # normal-sample cache
 
 
 def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
@@ -165,8 +166,12 @@ def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
     for i, (c, _b, kept) in enumerate(segs):
         if kept:
             offs[i], off = off, off + c
-    flat = torch.empty(off, dtype=torch.float32)
     raw = torch.get_rng_state().numpy().copy()
+    if raw.size != _STATE_BYTES or raw[_SEEDED].view(np.int32)[0] != 1:
+        # not the CPUGeneratorImplState layout this replay reads (another torch
+        # build): draw through the module itself, which is exact by definition
+        return SIREN(config, out_features).flat_parameters()
+    flat = torch.empty(off, dtype=torch.float32)
     state = raw[_STATE].view(np.uint64).astype(np.uint32)
     left = ctypes.c_int32(int(raw[_LEFT].view(np.int32)[0]))
     nxt = ctypes.c_uint32(int(raw[_NEXT].view(np.uint64)[0]))
