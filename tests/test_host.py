@@ -263,3 +263,92 @@ def test_uninitialised_draws_nothing():
     assert torch.equal(before, torch.get_rng_state())
     assert list(m.state_dict()) == list(SIREN(cfg, 128).state_dict())
     assert m.count_parameters() == cfg.num_parameters(128)
+
+
+class _FakeEvent:
+    def __init__(self, clock):
+        self.clock, self.t = clock, None
+
+    def record(self, _stream=None):
+        self.t = self.clock()
+
+    def query(self):
+        return self.t is not None
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
+def _fake_streaming(monkeypatch, rc=0):
+    """StreamingJob with the device side replaced by fakes (CPU only): the
+    launcher threads, the arrival-triggered launches, finished() and the error
+    path run for real; nerfhip_siren_fit returns `rc`."""
+    import itertools
+    import threading
+    import types
+    tick = itertools.count()
+    lock = threading.Lock()
+
+    def clock():
+        with lock:
+            return float(next(tick))
+
+    calls = []
+
+    class FakeGroup:
+        def __init__(self, members, specs, *a, **k):
+            self.members = members
+            self.stream = types.SimpleNamespace(cuda_stream=None)
+            self.desc = engine._native.NerfhipGroup()
+            self.ev_start, self.ev_end = _FakeEvent(clock), _FakeEvent(clock)
+
+        def outputs(self, specs, gs, job_s, job_f):
+            return [gs] * len(self.members)
+
+    class FakeLib:
+        def nerfhip_siren_fit(self, desc, n, st):
+            calls.append(threading.current_thread().name)
+            return rc
+
+        def nerfhip_status_string(self, code):
+            return b"launch failed"
+
+    lib = FakeLib()
+    monkeypatch.setattr(engine, "resolve_device", lambda d: types.SimpleNamespace(index=0))
+    monkeypatch.setattr(engine, "plan_groups", lambda protos, dev: [(0, [0, 2]), (0, [1])])
+    monkeypatch.setattr(engine, "_Group", FakeGroup)
+    monkeypatch.setattr(engine._native, "load", lambda path=None: lib)
+    cfg = SIRENConfig(64, 1, 30.0, "tiny")
+    protos = [engine.FitSpec(target=torch.zeros(4, 64), config=cfg, init=None) for _ in range(3)]
+    job = engine.StreamingJob(protos, 2, device=0, precision="bf16x3")
+    return job, protos, calls
+
+
+def test_streaming_job_launch_threads(monkeypatch):
+    """Each group is launched from its own thread as soon as its last fit
+    arrives (group 1 = fit 1 launches before group 0 = fits 0, 2 is complete);
+    finished() yields every group once, after its thread and end event."""
+    job, protos, calls = _fake_streaming(monkeypatch)
+    job.add(0, protos[0])
+    assert job.launch_order == []
+    job.add(1, protos[1])
+    assert job.launch_order == [1]
+    with pytest.raises(ValueError):
+        list(job.finished())                  # not every fit added yet
+    job.add(2, protos[2])
+    assert job.launch_order == [1, 0]
+    assert sorted(job.finished()) == [0, 1]
+    assert sorted(calls) == ["nerfhip-group-0", "nerfhip-group-1"]
+    assert [k for k, _ in job.outputs(0)] == [0, 2]
+    assert job.job_seconds() > 0
+    with pytest.raises(ValueError):
+        job.add(2, protos[2])                 # added twice
+
+
+def test_streaming_job_launch_error_surfaces(monkeypatch):
+    """A failing launch inside a launcher thread is raised by finished()."""
+    job, protos, _ = _fake_streaming(monkeypatch, rc=-6)
+    for i, p in enumerate(protos):
+        job.add(i, p)
+    with pytest.raises(engine._native.NerfhipError):
+        list(job.finished())
