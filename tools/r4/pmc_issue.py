@@ -4,16 +4,20 @@ sums per dispatch of k_step_rows<256, 128, true, true>, averaged over the
 dispatches.  Ratios: SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES (share of wave time
 waiting to issue an LDS instruction), SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES,
 instructions per wave-cycle by type.
-usage: python tools/r4/pmc_issue.py <counter_collection.csv> [...]"""
+usage: python tools/r4/pmc_issue.py [--kernel=<name prefix>] <counter_collection.csv> [...]"""
 import csv
 import json
 import re
 import sys
 from collections import defaultdict
 
-pat = re.compile(r"k_step_rows<256, 128, true, true")
+args = sys.argv[1:]
+kern = r"k_step_rows<256, 128, true, true"
+if args and args[0].startswith("--kernel="):
+    kern = re.escape(args.pop(0).split("=", 1)[1])
+pat = re.compile(kern)
 per = defaultdict(lambda: defaultdict(float))
-for path in sys.argv[1:]:
+for path in args:
     for r in csv.DictReader(open(path)):
         if not pat.search(r.get("Kernel_Name", "")):
             continue
