@@ -323,9 +323,47 @@ def _chunks(members: list, cap: int) -> list:
     return out
 
 
+XCDS = 8          # map_block (nerfhip.hip): fit k of a group of >= 8 runs on XCD k mod 8
+
+
+def xcd_order(members: list, costs: list) -> list:
+    """Permute one group's members so that every XCD carries the same work.
+
+    The kernels map fit k of a group (of at least 8 fits) to XCD k mod 8
+    (nerfhip.hip map_block: all tiles of a fit share an XCD's L2).  So the
+    position of a fit in its group decides its XCD, and a group laid out in
+    reference order puts every fit of a periodic pattern on the same XCDs —
+    in the sweep's W = 256 group (medium, deep, hifreq, lofreq repeating) all
+    deep fits had k = 1 mod 4, i.e. XCDs 1 and 5, which then held 1.4x the
+    work of the others.  Here: longest-first assignment of the
+    fits to the 8 XCD classes, each class holding exactly as many fits as
+    the positions k = x, x+8, ... that exist in a group of this size; then
+    fit j of class x goes to position x + 8j.  A fit's arithmetic does not
+    depend on its position (bitwise, test_xcd_order_bitwise), only the
+    placement changes."""
+    n = len(members)
+    if n < XCDS:
+        return list(members)
+    slots = [len(range(x, n, XCDS)) for x in range(XCDS)]
+    bins = [[] for _ in range(XCDS)]
+    load = [0.0] * XCDS
+    for i in sorted(members, key=lambda i: (-costs[i], i)):
+        x = min((x for x in range(XCDS) if len(bins[x]) < slots[x]), key=lambda x: (load[x], x))
+        bins[x].append(i)
+        load[x] += costs[i]
+    out = [None] * n
+    for x, b in enumerate(bins):
+        for j, i in enumerate(sorted(b)):
+            out[x + XCDS * j] = i
+    return out
+
+
+CHUNK_POLICIES = ("depth", "mixed", "spec")
+
+
 def plan_groups(specs: list, device: int) -> list:
     """[(device, [spec indices])] — fits grouped by (W, d, seq_len), large
-    groups chunked.
+    groups chunked, every chunk laid out XCD-balanced (xcd_order).
 
     A group's kernels depend on its size: bf16x3 groups of at most 128
     regular row workgroups run the K-split row kernel, and groups under 8
@@ -333,7 +371,9 @@ def plan_groups(specs: list, device: int) -> list:
     regroup the same sums, so a fit's result can differ at the rounding level
     (|Δcos| well under 1e-4) with the chunking or the farm partition that put
     it in a smaller or larger group; `test_group_chunks_row_variant_rounding`
-    pins that, `test_group_chunks_equal_one_group` the bitwise case."""
+    pins that, `test_group_chunks_equal_one_group` the bitwise case.
+    Records are written in the reference's order whatever the grouping:
+    outputs are indexed by spec."""
     costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
              for s in specs]
     keys = {}
@@ -351,9 +391,35 @@ def plan_groups(specs: list, device: int) -> list:
     # per-width override, e.g. NERFHIP_GROUP_MAX_512=8 (schedule experiments)
     caps = {w: int(v) for w, v in ((int(k.rsplit("_", 1)[1]), v) for k, v in os.environ.items()
                                    if k.startswith("NERFHIP_GROUP_MAX_"))}
+    # Which fits share a chunk (NERFHIP_CHUNKS):
+    #   depth  (default) chunks cut from the width's fits sorted by depth,
+    #          deepest first: the sweep's W = 256 group becomes one chunk of
+    #          40 deep (L = 3) fits and three of 40 L = 2 fits, so no chunk's
+    #          parameter grid carries dead layer-3 tiles for its L = 2 fits
+    #          (the grid is n_fits x tiles(L_max));
+    #   mixed  every chunk gets an equal share of each depth (dealt round
+    #          robin from the depth-sorted list);
+    #   spec   reference order (the round-4 plan; diagnostics).
+    policy = os.environ.get("NERFHIP_CHUNKS", "depth")
+    if policy not in CHUNK_POLICIES:
+        raise ValueError(f"NERFHIP_CHUNKS must be one of {CHUNK_POLICIES}, got {policy!r}")
     parts = []
     for k, m in keys.items():
-        parts += [(k[0], c) for c in _chunks(m, caps.get(k[1], cap))]
+        if policy != "spec":
+            m = sorted(m, key=lambda i: (-specs[i].config.hidden_layers, -costs[i], i))
+        chunks = _chunks(m, caps.get(k[1], cap))
+        if policy == "mixed" and len(chunks) > 1:
+            sizes = [len(c) for c in chunks]
+            dealt = [[] for _ in chunks]
+            at = 0
+            for i in m:
+                while len(dealt[at % len(chunks)]) >= sizes[at % len(chunks)]:
+                    at += 1
+                dealt[at % len(chunks)].append(i)
+                at += 1
+            chunks = dealt
+        for c in chunks:
+            parts.append((k[0], c if policy == "spec" else xcd_order(c, costs)))
     # heaviest groups first: they are enqueued (and start) first
     return sorted(parts, key=lambda dm: -sum(costs[i] for i in dm[1]))
 
@@ -568,6 +634,8 @@ class StreamingJob:
     def job_seconds(self) -> float:
         """Earliest group start to the last group's end (device clock)."""
         self._join_all()
+        if not self.groups:
+            return 0.0
         starts = [g.ev_start for g in self.groups]
         first = starts[0]
         for ev in starts[1:]:

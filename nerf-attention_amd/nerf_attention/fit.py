@@ -112,7 +112,11 @@ def _devices(device, gpus) -> list:
 
 
 def _stream_ok(plan, epochs, devices, log_every, precision) -> bool:
-    """The streaming path needs one device and one memory wave."""
+    """The streaming path needs one device, one memory wave and at least one
+    fit (an empty selection — every layer file missing — takes train_plan,
+    which returns no results, as the reference's loop does)."""
+    if not plan:
+        return False
     if devices is None or len(devices) != 1 or os.environ.get("NERFHIP_STREAM", "1") == "0":
         return False
     need = 0

@@ -367,3 +367,28 @@ def test_fitjob_threaded_launch_is_bitwise_equal(gpu, monkeypatch):
         outs[threads] = runs[0]
         del job
     assert all(torch.equal(a, b) for a, b in zip(outs[False], outs[True]))
+
+
+def test_xcd_order_bitwise(gpu, sweep, monkeypatch):
+    """The XCD-balanced, depth-sorted chunk plan (engine.plan_groups, default
+    NERFHIP_CHUNKS=depth) trains every sweep fit bitwise as the round-4 plan
+    (reference-order chunks, NERFHIP_CHUNKS=spec) does: parameters, every
+    epoch's loss and the final row cosines.  The plans really differ (the
+    W = 256 chunks change composition and every chunk's fit order), and the
+    outputs come back in spec (= reference record) order either way."""
+    _plan, specs = sweep
+    outs, plans = {}, {}
+    for policy in ("spec", "depth", "mixed"):
+        monkeypatch.setenv("NERFHIP_CHUNKS", policy)
+        job = engine.FitJob(specs, 60, devices=[0], precision="bf16x3")
+        plans[policy] = [list(m) for _d, m in job.plan]
+        job.launch()
+        job.wait()
+        outs[policy] = [(o.params.cpu(), o.losses, o.row_cos) for o in job.outputs()]
+        del job
+    assert plans["spec"] != plans["depth"] != plans["mixed"]
+    for policy in ("depth", "mixed"):
+        for k, (a, b) in enumerate(zip(outs["spec"], outs[policy])):
+            assert torch.equal(a[0], b[0]), (policy, k)
+            assert a[1] == b[1], (policy, k)
+            assert np.array_equal(a[2], b[2]), (policy, k)

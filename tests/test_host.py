@@ -113,6 +113,31 @@ def test_missing_layer_skipped():
     assert skipped == [2] and all(p[1] != 2 for p in plan)
 
 
+def test_fit_kv_cache_empty_selection(tmp_path, monkeypatch, capsys):
+    """Every selected layer file missing: the plan is empty, each layer prints
+    'Skipping layer' and fit_results.json is an empty list (fit.py:56-58,88-89)
+    — the streaming path is not taken for an empty plan.  The device is faked
+    (no GPU here); nothing reaches the engine."""
+    import types as pytypes
+    from nerf_attention import fit as fitmod
+    meta = types.KVMetadata("x", 4, 1, 8, 4, 8)
+    (tmp_path / "kv").mkdir()
+    (tmp_path / "kv" / "metadata.json").write_text(json.dumps(meta.to_dict()))
+    monkeypatch.setattr(engine, "resolve_device", lambda d: pytypes.SimpleNamespace(index=0))
+    monkeypatch.setattr(engine, "memory_budget", lambda dev: 1 << 40)
+    assert not fitmod._stream_ok([], 10, [0], 100, None)
+    out = fitmod.fit_kv_cache(tmp_path / "kv", tmp_path / "out", epochs=10, quick=True)
+    assert out == []
+    assert json.loads((tmp_path / "out" / "fit_results.json").read_text()) == []
+    assert capsys.readouterr().out.count("Skipping layer") == 3
+
+
+def test_streaming_job_seconds_without_groups():
+    job = object.__new__(engine.StreamingJob)
+    job.groups, job._threads = [], {}
+    assert job.job_seconds() == 0.0
+
+
 def _fake_output(cfg, N=16, D=8):
     torch.manual_seed(1)
     m = SIREN(cfg, D)
@@ -171,7 +196,8 @@ def test_plan_groups_by_width():
     specs = [engine.FitSpec(torch.zeros(128, 128), c, torch.zeros(1)) for c in cfgs]
     groups = engine.plan_groups(specs, 0)
     assert sorted(sorted(m) for _, m in groups) == [[0, 2, 3], [1]]
-    assert groups[0][1] == [0, 2, 3]          # heaviest first
+    assert sorted(groups[0][1]) == [0, 2, 3]          # heaviest first
+    assert groups[0][1][0] == 2                       # deepest first (NERFHIP_CHUNKS=depth)
 
 
 def test_non_hip_device_raises():
@@ -210,6 +236,47 @@ def test_plan_groups_chunks_large_groups():
     assert [len(c) for c in engine._chunks(list(range(100)), 40)] == [32, 32, 36]
     assert [len(c) for c in engine._chunks(list(range(9)), 40)] == [9]
     assert [len(c) for c in engine._chunks(list(range(160)), 0)] == [160]
+
+
+def _xcd_loads(members, costs):
+    return [sum(costs[i] for i in members[x::engine.XCDS]) for x in range(engine.XCDS)]
+
+
+@pytest.mark.parametrize("policy", ["depth", "mixed", "spec"])
+def test_sweep_chunks_xcd_balance(policy, monkeypatch):
+    """map_block puts fit k of a group on XCD k mod 8.  Reference order put
+    all 10 deep fits of every W = 256 chunk on XCDs 1 and 5 (max/mean XCD
+    work 1.27); the default plan cuts depth-uniform chunks
+    (one of 40 deep fits, three of 40 L = 2 fits: every XCD equal), 'mixed'
+    deals 10 deep fits to every chunk and spreads them over the XCDs."""
+    from nerf_attention.workloads import sweep_280
+    monkeypatch.setenv("NERFHIP_CHUNKS", policy)
+    _, specs = sweep_280(64, seed=0)
+    costs = [engine.fit_flops(2048, 128, s.config, 1) for s in specs]
+    groups = engine.plan_groups(specs, 0)
+    assert sorted(i for _, m in groups for i in m) == list(range(280))
+    w256 = [m for _, m in groups if specs[m[0]].config.hidden_features == 256]
+    assert [len(m) for m in w256] == [40] * 4
+    depths = sorted(tuple(sorted({specs[i].config.hidden_layers for i in m})) for m in w256)
+    imb = max(max(_xcd_loads(m, costs)) / (sum(costs[i] for i in m) / 8) for m in w256)
+    if policy == "spec":
+        assert imb == pytest.approx(1.2727, abs=1e-3)
+    elif policy == "depth":
+        assert depths == [(2,), (2,), (2,), (3,)]
+        assert imb == pytest.approx(1.0)
+    else:
+        assert all(sum(specs[i].config.hidden_layers == 3 for i in m) == 10 for m in w256)
+        assert imb < 1.06
+
+
+def test_xcd_order_balances_and_permutes():
+    costs = [1.0, 1.4, 1.0, 1.0] * 10 + [2.0] * 3
+    m = list(range(43))
+    out = engine.xcd_order(m, costs)
+    assert sorted(out) == m
+    loads = _xcd_loads(out, costs)
+    assert max(loads) - min(loads) <= 2.0
+    assert engine.xcd_order([3, 1, 2], costs) == [3, 1, 2]        # < 8 fits: linear map
 
 
 def test_param_tiles_matches_kernel_grid():

@@ -36,8 +36,9 @@ torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / args.steps
 secs = job.group_seconds()
 print(json.dumps({"tag": args.tag, "queues": os.environ.get("GPU_MAX_HW_QUEUES"),
-                  "group_max": os.environ.get("NERFHIP_GROUP_MAX", "40"), "epochs": args.epochs,
+                  "group_max": os.environ.get("NERFHIP_GROUP_MAX", "40"),
+                  "chunks": os.environ.get("NERFHIP_CHUNKS", "depth"), "epochs": args.epochs,
                   "s_per_sweep": round(dt, 4), "fits_per_s_2000ep_equiv":
                   round(280 / (dt * 2000 / args.epochs), 3),
-                  "groups": [[g.W, g.n, round(t, 3)] for g, t in zip(job.groups, secs)]}),
+                  "groups": [[g.W, g.n, g.L_max, round(t, 3)] for g, t in zip(job.groups, secs)]}),
       flush=True)
