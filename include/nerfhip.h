@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NERFHIP_ABI_VERSION 4
+#define NERFHIP_ABI_VERSION 5
 
 typedef enum nerfhip_status {
   NERFHIP_OK = 0,
@@ -166,8 +166,10 @@ int nerfhip_siren_forward(const nerfhip_group* g, void* stream);
  * the group's shape fields, precision and whether grad_partial is set). */
 typedef enum nerfhip_rows_variant {
   NERFHIP_ROWS_REGULAR = 0,   /* k_step_rows: 64-row workgroups, one wave per 16 rows     */
-  NERFHIP_ROWS_KSPLIT = 1     /* k_step_rows_ks: four waves split every GEMM's k over one
+  NERFHIP_ROWS_KSPLIT = 1,    /* k_step_rows_ks: four waves split every GEMM's k over one
                                  16-row block (small bf16x3 groups, W >= 128, D = 128)   */
+  NERFHIP_ROWS_32 = 2         /* k_step_rows32: 128-row workgroups, one wave per 32 rows,
+                                 32x32x16 MFMAs (bf16x3, W = 256, D = 128, n_pad % 128 = 0) */
 } nerfhip_rows_variant;
 
 typedef struct nerfhip_plan {
@@ -180,6 +182,15 @@ typedef struct nerfhip_plan {
 } nerfhip_plan;
 
 int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out);
+
+/* Diagnostic compile-time switches this library was built with (0 for a
+ * product build): bit 0 any NERFHIP_EXP_* timing/diagnostic macro (such
+ * builds may compute wrong results on purpose), bit 1 NERFHIP_STAMPS
+ * (in-kernel timestamps), bit 2 NERFHIP_DIAG_* (altered launch sequence). */
+#define NERFHIP_BUILD_EXP 1
+#define NERFHIP_BUILD_STAMPS 2
+#define NERFHIP_BUILD_DIAG 4
+int nerfhip_build_flags(void);
 
 /* ------------------------------------------------------------------------
  * Truncated-SVD baseline (BASELINE config 5).

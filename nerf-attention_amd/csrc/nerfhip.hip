@@ -91,6 +91,8 @@ struct KArgs {
   uint16_t* wsplit;
   // row-step variant: 1 = the K-split kernel for small groups (k_step_rows_ks)
   int32_t rows_ks;
+  // 1 = the 32-row kernel (k_step_rows32; bf16x3, W = 256, D = 128)
+  int32_t rows32;
   // split-K parameter step on 64 × 64 tiles (ParamsCfg SMALL; split_for)
   int32_t small_tiles;
   // diagnostic builds only (NERFHIP_STAMPS): per-wave s_memrealtime stamps of
@@ -103,6 +105,7 @@ struct KArgs {
 };
 template <int W, int D, bool X3> int launch_rows(const KArgs& a, hipStream_t st);
 template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t st);
+template <int W, int D> int launch_rows32(const KArgs& a, hipStream_t st);
 }  // namespace nerfhip_detail
 
 namespace {
@@ -132,6 +135,19 @@ __device__ unsigned long long* g_stamps = nullptr;
       g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] += (v); \
   } while (0)
 #define MEMTIME() __builtin_amdgcn_s_memtime()
+// the 32-row kernel's stamps: [blocks][4 waves][32] from a.pstamps + 262144
+// (after the parameter and K-split kernels' regions), through a pointer the
+// kernel hands to its phases (g_stamps is per translation unit)
+#define R32STAMP_ADD(p, k, v)                                                          \
+  do {                                                                                 \
+    if ((p) && (threadIdx.x & 63) == 0)                                                \
+      (p)[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (k)] += (v);            \
+  } while (0)
+#define R32STAMP(p, k)                                                                 \
+  do {                                                                                 \
+    if ((p) && (threadIdx.x & 63) == 0)                                                \
+      (p)[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #define PSTAMP(k)                                                                      \
   do {                                                                                 \
     if (a.pstamps && (threadIdx.x & 63) == 0)                                          \
@@ -146,6 +162,12 @@ __device__ unsigned long long* g_stamps = nullptr;
           __builtin_amdgcn_s_memrealtime();                                            \
   } while (0)
 #else
+#define R32STAMP_ADD(p, k, v) \
+  do {                        \
+  } while (0)
+#define R32STAMP(p, k) \
+  do {                 \
+  } while (0)
 #define PSTAMP(k) \
   do {            \
   } while (0)
@@ -418,8 +440,25 @@ __host__ __device__ inline int64_t xoff_ks(int K, int r, int k, int plane) {
   return ((((int64_t)(r >> 4) * (K >> 5) + (k >> 5)) * 3 + plane) << 9) + ((r & 15) << 5) +
          kperm(k & 31);
 }
-__host__ __device__ inline int64_t xoff_any(bool ks, int R, int K, int r, int k, int plane) {
-  return ks ? xoff_ks(K, r, k, plane) : xoff(R, K, r, k, plane);
+// The 32-row kernel's layout (groups that run k_step_rows32, KArgs::rows32):
+// [R/32][K/128][3 planes][32 rows][128] — one 32-row × 128-k sub-chunk of all
+// three planes is one contiguous 24 KB run (its LDS-DMA unit) — with the k
+// order inside every 16-deep k-step permuted to the 32 × 32 × 16 MFMA
+// operand order: stored position 8h + j of a lane half h holds feature
+// 8(j>>2) + 4h + (j&3), the order in which the 32 × 32 accumulator tile of
+// the layer before hands a lane its next-layer B fragment.
+__host__ __device__ inline int perm32(int f) {   // f in [0, 16)
+  return 8 * ((f >> 2) & 1) + 4 * (f >> 3) + (f & 3);
+}
+__host__ __device__ inline int64_t xoff32(int K, int r, int k, int plane) {
+  return ((((int64_t)(r >> 5) * (K >> 7) + (k >> 7)) * 3 + plane) * 32 + (r & 31)) * 128 +
+         (k & 127 & ~15) + perm32(k & 15);
+}
+// weight-plane layouts (KArgs: rows_ks → xoff_ks, rows32 → xoff32, else xoff)
+constexpr int kLayX = 0, kLayKs = 1, kLay32 = 2;
+__host__ __device__ inline int64_t xoff_any(int lay, int R, int K, int r, int k, int plane) {
+  return lay == kLayKs ? xoff_ks(K, r, k, plane)
+                       : lay == kLay32 ? xoff32(K, r, k, plane) : xoff(R, K, r, k, plane);
 }
 // per-fit split matrices: forward M_i [out][in] for i = 1..L (hidden) and
 // i = L+1 (final, [D][W]), then the transposed M_iᵀ the backward streams
@@ -431,7 +470,7 @@ __host__ __device__ inline int64_t xs_size(int W, int D, int L) {
   return 6 * ((int64_t)L * W * W + (int64_t)D * W);
 }
 // weight element M_i[j][k] = p into both split copies (prologue / split-K)
-__device__ __forceinline__ void put_w(uint16_t* XS, bool ks, int W, int D, int L, int i, int j,
+__device__ __forceinline__ void put_w(uint16_t* XS, int ks, int W, int D, int L, int i, int j,
                                       int k, float p) {
   const int R = i <= L ? W : D;
   uint32_t h, m, l;
@@ -473,6 +512,10 @@ __device__ __forceinline__ bool map_block(int b, int n_fits, int n_tiles, int& f
 // decode of a lone fit's kernels (config 2's launches are latency-bound)
 __device__ __forceinline__ int fit_layers_of(const KArgs& a, int fit) {
   return a.n_fits == 1 ? a.L_max : a.fit_layers[fit];
+}
+// the weight-plane layout the group's row kernel reads
+__host__ __device__ inline int wlayout(const KArgs& a) {
+  return a.rows_ks ? kLayKs : a.rows32 ? kLay32 : kLayX;
 }
 
 __host__ __device__ inline int64_t off_hidden_w(int W, int i) {  // i = 1..L
@@ -1576,6 +1619,574 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// 32-row row step (bf16x3; W = 256, D = 128): k_step_rows32.
+//
+// k_step_rows' contract — the same scratch (H, dZ, G row-block-major, the
+// dZ0 partials, the loss partials), so the parameter kernel is shared — with
+// every GEMM on v_mfma_f32_32x32x16_bf16 over 32 data rows per wave:
+//  * one A fragment (a 32-feature × 16-k weight slice, three planes) feeds
+//    32 rows instead of 16, and four waves × 32 rows share one staged copy of
+//    the weights: LDS fragment reads and LDS-DMA staging per FLOP halve;
+//  * a 32 × 32 × 16 MFMA holds its SIMD's vector issue for 8 of its 32
+//    cycles, a 16 × 16 × 32 one for 8 of 16: 1.5x the free VALU issue per
+//    FLOP for the sincos / split epilogue (MI355X_MICROARCH.md cycle table);
+//  * the layer input — the B operand, 32 rows × W k in three planes, 192
+//    registers at W = 256 — lives in the accumulator registers (AGPRs), which
+//    gfx950 MFMAs read as sources (to_agpr); the layer output (128 VGPRs) and
+//    the accumulators stay in VGPRs (this kernel's translation unit is built
+//    with -amdgpu-mfma-vgpr-form, _build.py).  One wave per SIMD.
+// Orientation as k_step_rows (Zᵀ = W·Hᵀ).  The 32 × 32 accumulator tile of
+// output features 32J.. holds, in lane (row j = lane & 31, h = lane >> 5),
+// register e = feature 32J + 8(e>>2) + 4h + (e&3) of row j; registers
+// 8s..8s+7 are exactly the next layer's B fragment of k-step 2J + s under
+// the k order perm32 (cdna_hip_programming.md §3), which the weight planes
+// use (xoff32, written by the Adam epilogue and the prologue).
+// The k sums are grouped differently from k_step_rows (32 × 32 × 16 instead
+// of 16 × 16 × 32 MFMAs), so the two agree to rounding, not bitwise
+// (test_rows32_matches_regular).
+// ---------------------------------------------------------------------------
+template <int K> struct R32Cfg {
+  static constexpr int KC = 128, NH = K / KC, KT = KC / 16;   // sub-chunk: 32 rows × KC
+  static constexpr int CH = 3 * 32 * KC;                       // bf16 per ring buffer (24 KB)
+  static constexpr int PLB = 2 * 32 * KC;                      // bytes per plane
+  static constexpr int NDMA = 3 * 32 * (KC / 8) / 256;         // DMAs per wave and sub-chunk
+  static_assert(K % KC == 0, "rows32: K must be a multiple of 128");
+};
+// sub-chunk buffers of the LDS ring: sub-chunk u + NR32 - 1 is issued at the
+// top of sub-chunk u and waited for at the end of u + NR32 - 2
+#ifndef NERFHIP_R32_RING
+#define NERFHIP_R32_RING 3
+#endif
+constexpr int NR32 = NERFHIP_R32_RING;
+static_assert(NR32 >= 3, "rows32 ring: at least 3 buffers");
+constexpr int kRing32 = NR32 * R32Cfg<128>::CH;
+
+// a B fragment moved into accumulator registers: an MFMA reads it from there
+// directly (the compiler emits the v_accvgpr_write copies and the hazards)
+__device__ __forceinline__ S8 to_agpr(const S8& v) {
+  S8 r;
+  asm("" : "=a"(r.h) : "0"(v.h));
+  asm("" : "=a"(r.m) : "0"(v.m));
+  asm("" : "=a"(r.l) : "0"(v.l));
+  return r;
+}
+
+// LDS-DMA of sub-chunk u (a 32-row × 128-k slice of all three planes, one
+// contiguous 24 KB run of the xoff32 layout) of the matrix at src into ring
+// slot u % NR32.  Round m moves physical slots tid + 256m (16 slots per row):
+// row tid/16 + 16m of the [3][32] plane rows, slot tid % 16; its swizzle
+// (row & 15 = tid/16) is the same in every round, so one per-lane source
+// offset serves all rounds (+16m rows: a compile-time addend).  The DMA
+// image is lane-linear; the bank swizzle (16-B slot s of row r at
+// s ^ (r & 15)) lives on the source address.
+struct R32Dma {
+  static constexpr int KC = 128, CH = 3 * 32 * KC, NDMA = 6;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff, wave;
+  __device__ __forceinline__ R32Dma(const uint16_t* src, int tid)
+      : rsrc(__builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000)),
+        voff(2 * ((tid >> 4) * KC + 8 * ((tid & 15) ^ (tid >> 4)))),
+        wave(__builtin_amdgcn_readfirstlane(tid >> 6)) {}
+  template <int U> __device__ __forceinline__ void issue(uint16_t* ring) const {
+    typedef __attribute__((address_space(3))) void lds_void;
+    uint16_t* buf = ring + (U % NR32) * CH;
+    static_for<0, NDMA>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(buf + 8 * (256 * m + 64 * wave)),
+                                               16, voff, 2 * U * CH + 32 * m * KC, 0, 0);
+    });
+  }
+};
+// a phase's first NR32 - 1 sub-chunks, issued ahead of it (by the previous
+// phase right after its last barrier, or by the kernel before layer 0)
+__device__ __forceinline__ void r32_prefetch(const uint16_t* src, uint16_t* ring, int tid) {
+  const R32Dma d(src, tid);
+  static_for<0, NR32 - 1>([&](auto uc) { d.template issue<decltype(uc)::value>(ring); });
+}
+
+// One GEMM phase Zᵀ[32·JT][32 rows] = M[32·JT][K] · Hᵀ of the 32-row kernel
+// (gemm_phase_x3's pipeline on 32-row sub-chunks): sub-chunk u = J·NH + hh
+// (output tile J, k-chunk hh) of the xoff32 planes arrives by LDS-DMA into an
+// NR32-deep ring NR32 - 1 sub-chunks ahead; each of its KT k-steps is three
+// ds_read_b128 (one per plane; every 16-lane group reads one bank row once)
+// and six 32 × 32 × 16 MFMAs.
+//   pre(J)      issues tile J's per-lane loads at the top of tile J;
+//   epre(J, ep) issues tile J's NEP epilogue operands from LDS (bias, w0 / b0:
+//               inline-asm ds_read_b128 into ep) together with the first A
+//               fragment of tile J+1, so they land in that fragment's wait —
+//               a compiler-placed LDS read inside the k-steps would get an
+//               lgkmcnt(0) that also waits for the next k-step's fragments
+//               and exposes their latency at every k-step;
+//   elem(J, e, ep)  epilogue of element e of tile J, spread over tile J+1's
+//               k-steps (16 / (KT·NH) per k-step);
+//   done(J, hi, lo)  hands over tile J's accumulators at its end;
+//   flush(J)    tile J's stores, at the top of tile J+2.
+// NST / NLD: the exact store / load instruction counts of flush / pre (or
+// fewer: fewer only over-waits), as in gemm_phase_x3.
+// Phase boundaries.  The phase's first NR32 - 1 sub-chunks were issued before
+// it (r32_prefetch), followed by NAFTER vector-memory ops (the previous
+// phase's last two flushes, or layer 0's stores; fewer only over-waits), and
+// the phase issues the NEXT phase's first sub-chunks (`next`, nullptr: none)
+// right after its last barrier, before its own last epilogue and stores: the
+// in-order vmcnt then never makes a phase's first wait cover the previous
+// phase's stores.  (With each phase issuing its own first sub-chunks, and the
+// bias loaded from global memory at every phase, the compiler's vmcnt(0) for
+// that load and the end-of-phase waits drained every store and exposed the
+// first sub-chunk's latency: ≈30 K of a wave's ≈480 K cycles per phase,
+// profiles/r05/stamps32_*.log.)
+// The B operand b[k-step] is split from the previous layer's f32 output
+// tiles `hs` lazily, one k-step ahead, inside tile 0 (whose k-steps carry no
+// epilogue): hs (the caller's output array) is rewritten only from the end
+// of tile 0 on.  Split between the phases instead, ≈1,100 VALU per phase
+// (128 elements and 192 accumulator-register writes) ran with nothing to
+// overlap at one wave per SIMD.
+template <int K, int JT, int NST, int NLD, int NEP, int NAFTER, int NB, int NTS, class Pre,
+          class Epre, class Elem, class Done, class Flush>
+__device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
+                                       const uint16_t* __restrict__ next, uint16_t* ring,
+                                       S8 (&b)[NB], const float (&hs)[NTS][16], int tid,
+                                       int lane, Pre&& pre, Epre&& epre, Elem&& elem,
+                                       Done&& done, Flush&& flush,
+                                       unsigned long long* stp = nullptr, int sslot = 8) {
+  using C = R32Cfg<K>;
+  constexpr int NH = C::NH, KT = C::KT, U = JT * NH, CH = C::CH, PLB = C::PLB;
+  constexpr int NDMA = C::NDMA, EPK = 16 / (KT * NH);
+  static_assert(NB >= K / 16 && 2 * NTS >= K / 16 && EPK * KT * NH == 16, "rows32 phase shape");
+  static_assert(NDMA == R32Dma::NDMA && CH == R32Dma::CH && U >= NR32 - 1, "rows32 DMA shape");
+  constexpr int KS = K / 16;   // k-steps of the B operand
+  auto split_b = [&](auto kc) {
+    constexpr int kk = decltype(kc)::value;
+    float x8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x8[e] = hs[kk >> 1][8 * (kk & 1) + e];
+    b[kk] = to_agpr(split8(x8));
+  };
+  const R32Dma dm(src, tid);
+  // lane (row j, half h): k-step kt reads logical slot 2kt + h of row j
+  const int j = lane & 31;
+  const uint32_t arow = lds_addr(ring) + 2 * C::KC * j;
+  const uint32_t ax = (uint32_t)(((lane >> 5) ^ (j & 15)) << 4);
+  auto aread = [&](auto uc, auto ktc) {
+    constexpr int OFF = (decltype(uc)::value % NR32) * 2 * CH;
+    constexpr int kt = decltype(ktc)::value;
+    const uint32_t ad = arow + (((uint32_t)kt << 5) ^ ax);
+    S8 r;
+    if constexpr (OFF + 2 * PLB < 65536) {
+      r.h = ds_read16<OFF>(ad);
+      r.m = ds_read16<OFF + PLB>(ad);
+      r.l = ds_read16<OFF + 2 * PLB>(ad);
+    } else {
+      const uint32_t ad2 = ad + OFF;
+      r.h = ds_read16<0>(ad2);
+      r.m = ds_read16<PLB>(ad2);
+      r.l = ds_read16<2 * PLB>(ad2);
+    }
+    return r;
+  };
+  auto lgkm_wait = [](S8& r) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r.h), "+v"(r.m), "+v"(r.l));
+  };
+  u4 ep[NEP > 0 ? NEP : 1];
+  auto ep_wait = [&]() {   // the epilogue operands land with the fragment wait
+#pragma unroll
+    for (int i = 0; i < NEP; ++i) asm volatile("" : "+v"(ep[i]));
+  };
+  auto vm_wait_barrier = [&](auto nc) {
+    if constexpr (decltype(nc)::value >= 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(decltype(nc)::value));
+    asm volatile("s_waitcnt lgkmcnt(0)");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // vector-memory ops issued after sub-chunk d's DMA and before the wait for
+  // it at the end of iteration d - 1 (d = 0: the phase's first wait), in the
+  // issue order [prefetch DMA 0 .. NR32-2][NAFTER][iteration 0: flush, pre,
+  // DMA(NR32-1)][iteration 1] ...
+  auto younger = [](int d, int upto) {   // ops issued after DMA(d), up to iteration `upto`
+    int n = 0;
+    if (d < NR32 - 1) n += (NR32 - 2 - d) * NDMA + NAFTER;   // rest of the prefetch, NAFTER
+    const int v0 = d < NR32 - 1 ? 0 : d - NR32 + 2;          // iterations after DMA(d)'s own
+    for (int v = v0; v <= upto; ++v) {
+      if (v % NH == 0) n += NLD + (v / NH >= 2 ? NST : 0);
+      if (v + NR32 - 1 < U && v + NR32 - 1 != d) n += NDMA;
+    }
+    return n;
+  };
+  const unsigned long long t_p0 = MEMTIME();
+  vm_wait_barrier(std::integral_constant<int, younger(0, -1)>{});   // sub-chunk 0 landed
+  const unsigned long long t_p1 = MEMTIME();
+  split_b(ic<0>);
+  S8 a_cur = aread(ic<0>, ic<0>);
+  lgkm_wait(a_cur);
+#ifdef NERFHIP_STAMPS
+  R32STAMP_ADD(stp, 29, t_p1 - t_p0);          // phase heads: wait for sub-chunk 0
+  R32STAMP_ADD(stp, 30, MEMTIME() - t_p1);     // phase heads: first split + fragment
+#else
+  (void)t_p0; (void)t_p1;
+#endif
+  f16v hi, lo;
+  static_for<0, U>([&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    constexpr int J = u / NH, hh = u % NH;
+    const unsigned long long t_f0 = MEMTIME();
+    if constexpr (hh == 0) {
+      if constexpr (J >= 2) flush(ic<J - 2>);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        hi[e] = 0.f;
+        lo[e] = 0.f;
+      }
+      pre(ic<J>);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // flush / pre before the DMA: vmcnt counts in order
+    const unsigned long long t_d0 = MEMTIME();
+    if constexpr (u + NR32 - 1 < U) dm.template issue<u + NR32 - 1>(ring);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long t_d1 = MEMTIME();
+    static_for<0, KT>([&](auto ktc) {
+      constexpr int kt = decltype(ktc)::value;
+      S8 a_nxt = a_cur;
+      if constexpr (kt + 1 < KT) a_nxt = aread(uc, ic<kt + 1>);
+      if constexpr (J == 0 && hh * KT + kt + 1 < KS) split_b(ic<hh * KT + kt + 1>);
+      mfma32x3(a_cur, b[hh * KT + kt], hi, lo);
+      if constexpr (J > 0) {
+        static_for<0, EPK>([&](auto ec) {
+          elem(ic<J - 1>, ic<(hh * KT + kt) * EPK + decltype(ec)::value>, ep);
+        });
+      }
+      if constexpr (kt + 1 < KT) lgkm_wait(a_nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      a_cur = a_nxt;
+    });
+    if constexpr (hh == NH - 1) done(ic<J>, hi, lo);
+    const unsigned long long t_w0 = MEMTIME();
+    // sub-chunk u+1 landed everywhere (the last iteration waits for no DMA:
+    // its barrier only frees the ring for the next phase's prefetch)
+    vm_wait_barrier(std::integral_constant<int, (u + 1 < U ? younger(u + 1, u) : -1)>{});
+#ifdef NERFHIP_STAMPS
+    const unsigned long long t_w1 = MEMTIME();
+    R32STAMP_ADD(stp, sslot, t_d1 - t_d0);      // DMA issue
+    R32STAMP_ADD(stp, sslot + 1, t_w0 - t_d1);  // k-steps (MFMA + epilogue VALU + LDS reads + split)
+    R32STAMP_ADD(stp, sslot + 2, t_w1 - t_w0);  // vm wait + barrier
+    R32STAMP_ADD(stp, sslot + 3, 1ull);         // sub-chunks
+    R32STAMP_ADD(stp, 31, t_d0 - t_f0);         // flush + pre (all phases)
+#else
+    (void)t_d0; (void)t_d1; (void)t_w0; (void)stp; (void)sslot; (void)t_f0;
+#endif
+    if constexpr (u + 1 < U) {
+      // tile J's epilogue operands, read now for its epilogue in tile J+1
+      if constexpr (NEP > 0 && (u + 1) % NH == 0) epre(ic<J>, ep);
+      a_cur = aread(ic<u + 1>, ic<0>);
+      lgkm_wait(a_cur);
+      if constexpr (NEP > 0 && (u + 1) % NH == 0) ep_wait();
+    }
+#ifdef NERFHIP_STAMPS
+    R32STAMP_ADD(stp, 27, MEMTIME() - t_w1);    // first fragment of the next sub-chunk
+#endif
+  });
+  if (next) r32_prefetch(next, ring, tid);   // (wave-uniform)
+  const unsigned long long t_e0 = MEMTIME();
+  if constexpr (JT >= 2) flush(ic<JT - 2>);
+  if constexpr (NEP > 0) {
+    epre(ic<JT - 1>, ep);
+    asm volatile("s_waitcnt lgkmcnt(0)");
+    ep_wait();
+  }
+  static_for<0, 16>([&](auto ec) { elem(ic<JT - 1>, ec, ep); });
+  flush(ic<JT - 1>);
+#ifdef NERFHIP_STAMPS
+  R32STAMP_ADD(stp, 28, MEMTIME() - t_e0);   // phase tails
+#else
+  (void)t_e0;
+#endif
+}
+
+template <int W, int D, bool TRAIN>
+__global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
+  static_assert(W == 256 && (D == 128), "rows32: W = 256, D = 128");
+  constexpr int JW = W / 32, JD = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t ring[kRing32];
+  // every bias of the fit, staged once: w0 ‖ b0 ‖ b_1 .. b_L ‖ b_f
+  __shared__ __attribute__((aligned(16))) float bias[(2 + NERFHIP_MAX_LAYERS) * W + D];
+  int fit, tile;
+  if (!map_block(blockIdx.x, a.n_fits, a.n_pad / 128, fit, tile)) return;
+#ifdef NERFHIP_STAMPS
+  unsigned long long* const stp = a.pstamps && TRAIN ? a.pstamps + 262144 : nullptr;
+#else
+  unsigned long long* const stp = nullptr;
+#endif
+  R32STAMP(stp, 0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, h = lane >> 5;
+  const int L = fit_layers_of(a, fit);
+  const float om = a.fit_omega[fit];
+  const int n_pad = a.n_pad;
+  const int r0 = tile * 128 + 32 * wave;       // the wave's first row
+  const int r = r0 + j;                        // this lane's row (B / D column)
+  const bool valid = r < a.N;
+  constexpr bool train = TRAIN;
+  const float* P = a.params + fit * a.p_stride;
+  float* S = a.scratch + fit * a.s_stride;
+  const int64_t WN = (int64_t)W * n_pad;
+  float* SH = S;
+  float* SZ = S + (int64_t)(a.L_max + 1) * WN;
+  float* SG = S + 2 * (int64_t)(a.L_max + 1) * WN;
+  float* SC = SG + (int64_t)D * n_pad;
+  const uint16_t* XS = a.wsplit + fit * a.ws_stride;
+  // row-block-major stores after quad_transpose: lane (j = 4a + b, h) writes
+  // feature 32J + 8t + 4h + b of rows 4a..4a+3 (16 contiguous bytes)
+  const int blk = (r0 >> 4) + (j >> 4);        // this lane's 16-row block
+  const int tq = (4 * h + (j & 3)) * 16 + 4 * ((j >> 2) & 3);
+  float* SHt = SH + (int64_t)blk * W * 16 + tq;
+  float* SZt = SZ + (int64_t)blk * W * 16 + tq;
+  float* SGt = SG + (int64_t)blk * D * 16 + tq;
+  // private cos map [n_pad/32][W/32][4][64 lanes][4]: one 1 KB run per (tile, t)
+  const int64_t coff = (int64_t)(r0 >> 5) * JW * 4 * 256 + lane * 4;
+  auto tile_store = [&](float* base, auto Jc, const float (&v)[16]) {
+    constexpr int J = decltype(Jc)::value;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f4 x = {v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
+      sst4(base + (32 * J + 8 * t) * 16, quad_transpose(x, j));
+    }
+  };
+  // (element e of a tile is feature 32J + 8(e>>2) + 4h + (e&3))
+  float ho[JW][16];    // a layer's output tiles (raw accumulators until their epilogue)
+  S8 hb[W / 16];       // the layer input as split k-steps, in AGPRs
+  auto done = [&](auto Jc, const f16v& hi, const f16v& lo) {
+    constexpr int J = decltype(Jc)::value;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) ho[J][e] = hi[e] + lo[e];
+  };
+  auto no_pre = [](auto) {};
+  auto no_epre = [](auto, auto&) {};
+  auto xsm = [&](bool bwd, int i) { return XS + xs_mat(W, D, L, bwd, i); };
+  // a tile's 16 epilogue constants from LDS (bias: ep[t][q] = bias[bo + 32J + 8t + 4h + q])
+  const uint32_t bias_lane = lds_addr(bias) + 16 * h;
+  auto bias_epre = [&](uint32_t bo) {
+    const uint32_t base = bias_lane + 4 * bo;
+    return [base](auto Jc, u4 (&ep)[4]) {
+      constexpr int J = decltype(Jc)::value;
+      static_for<0, 4>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        ep[t] = ds_read16<(32 * J + 8 * t) * 4>(base);
+      });
+    };
+  };
+  auto epv = [](const u4* ep, int e) { return __uint_as_float(ep[e >> 2][e & 3]); };
+
+  // ---- every bias once (nothing is in flight yet, so the compiler's vmcnt(0)
+  // for these loads drains nothing), then the first hidden phase's weights
+  {
+    const int nb = (2 + L) * W + D;
+    for (int i = tid; i < nb; i += 256) {
+      float v;
+      if (i < 2 * W) v = P[i];
+      else if (i < (2 + L) * W) v = P[off_hidden_w(W, (i - 2 * W) / W + 1) + W * W + (i % W)];
+      else v = P[off_final_w(W, L) + W * D + (i - (2 + L) * W)];
+      bias[i] = v;
+    }
+  }
+  __syncthreads();
+  r32_prefetch(xsm(false, 1), ring, tid);
+
+  // ---- layer 0: SineLayer(1, W, is_first), K = 1 (VALU), in the accumulator layout
+  const float x = a.pos[r];
+  static_for<0, JW>([&](auto Tc) {
+    constexpr int T = decltype(Tc)::value;
+    u4 wb[8];        // w0, b0 of the tile's 16 features (inline-asm reads: no vmcnt drain
+                     // of the prefetch in flight, as a compiler-visible LDS read would get)
+    static_for<0, 4>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      wb[t] = ds_read16<(32 * T + 8 * t) * 4>(bias_lane);
+      wb[4 + t] = ds_read16<(W + 32 * T + 8 * t) * 4>(bias_lane);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]), "+v"(wb[3]),
+                 "+v"(wb[4]), "+v"(wb[5]), "+v"(wb[6]), "+v"(wb[7]));
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float z = __fadd_rn(__fmul_rn(x, epv(wb, e)), epv(wb + 4, e));
+      float s, co;
+      sincos_fast(__fmul_rn(om, z), &s, &co);
+      ho[T][e] = s;
+    }
+    if (train) tile_store(SHt, Tc, ho[T]);
+  });
+  R32STAMP(stp, 1);
+
+  // ---- hidden SineLayers 1..L: Zᵀ = Wᵢ·Hᵀ (+b), H = sin(ωZ); each phase
+  // prefetches the next (hidden i+1, or the final layer's W_f = matrix L + 1)
+  for (int i = 1; i <= L; ++i) {
+    float* SHi = SHt + (int64_t)i * WN;
+    float* SCi = SC + (int64_t)i * WN + coff;
+    float cp[16];
+    gemm32<W, JW, TRAIN ? 8 : 0, 0, 4, TRAIN ? 16 : 0>(
+        xsm(false, i), xsm(false, i + 1), ring, hb, ho, tid, lane, no_pre,
+        bias_epre((uint32_t)((1 + i) * W)),
+        [&](auto Jc, auto ec, const auto& ep) {
+          constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
+          const float z = __fadd_rn(ho[J][e], epv(ep, e));
+          float s, co;
+          sincos_fast(__fmul_rn(om, z), &s, &co);
+          ho[J][e] = s;
+          cp[e] = co;
+        },
+        done,
+        [&](auto Jc) {
+          constexpr int J = decltype(Jc)::value;
+          if (train) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const f4 v = {cp[4 * t], cp[4 * t + 1], cp[4 * t + 2], cp[4 * t + 3]};
+              cst4(SCi + (J * 4 + t) * 256, v);
+            }
+            tile_store(SHi, Jc, ho[J]);
+          }
+        }, stp, 8);
+  }
+
+  // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f ; MSE ; dL/dŷ
+  R32STAMP(stp, 2);
+  const float* T = a.tnorm + fit * a.t_stride + (int64_t)r * D + 4 * h;
+  // wave-uniform scalar test (no EXEC write near the tile stores)
+  const bool has_y = a.y_out != nullptr;
+  float* yo = has_y ? a.y_out + fit * a.y_stride + (int64_t)r * D + 4 * h : nullptr;
+  float pv[2][16];     // per-lane operands of tiles J (J & 1), loaded a tile ahead
+  float yp[16];
+  float sq = 0.f;
+  gemm32<W, JD, TRAIN ? 4 : 0, TRAIN ? 4 : 0, 4, TRAIN ? 16 : 0>(
+      xsm(false, L + 1), train ? xsm(true, L + 1) : nullptr, ring, hb, ho, tid, lane,
+      [&](auto Jc) {
+        constexpr int J = decltype(Jc)::value;
+        if (train) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const f4 v = ld4(T + 32 * J + 8 * t);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pv[J & 1][4 * t + q] = v[q];
+          }
+        }
+      },
+      bias_epre((uint32_t)((2 + L) * W)),
+      [&](auto Jc, auto ec, const auto& ep) {
+        constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
+        const float y = __fadd_rn(ho[J][e], epv(ep, e));
+        yp[e] = y;
+        if (train) {
+          const float diff = y - pv[J & 1][e];
+          sq = valid ? fmaf(diff, diff, sq) : sq;
+          ho[J][e] = valid ? a.grad_scale * diff : 0.f;
+        }
+      },
+      done,
+      [&](auto Jc) {
+        constexpr int J = decltype(Jc)::value;
+        if (has_y) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const f4 v = {yp[4 * t], yp[4 * t + 1], yp[4 * t + 2], yp[4 * t + 3]};
+            st4(yo + 32 * J + 8 * t, v);      // ŷ[r][32J + 8t + 4h + q]
+          }
+        }
+        if (train) tile_store(SGt, Jc, ho[J]);
+      }, stp, 12);
+  R32STAMP(stp, 3);
+  if (!train) return;
+  // loss partials per 16-row block: lanes 0..15 (and their h = 1 partners)
+  // hold the wave's first block, lanes 16..31 its second
+  sq += __shfl_xor(sq, 32, 64);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);
+  if ((lane & 47) == 0)                          // lanes 0 and 16
+    a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + blk] = sq;
+
+  // ---- backward: dZ = (dH ⊙ cos(ωz))·ω, stored for the weight gradients
+  // (the phase after W_iᵀ is W_{i-1}ᵀ, down to W_1ᵀ = xsm(true, 1), whose
+  // phase is layer 0's; NAFTER: the previous phase's last two G or dZ flushes)
+  auto bwd = [&](const uint16_t* Mt, const uint16_t* next, auto Kc, int layer) {
+    constexpr int K = decltype(Kc)::value;
+    const float* SCl = SC + (int64_t)layer * WN + coff;
+    float* SZl = SZt + (int64_t)layer * WN;
+    gemm32<K, JW, 4, 4, 0, 8>(
+        Mt, next, ring, hb, ho, tid, lane,
+        [&](auto Jc) {
+          constexpr int J = decltype(Jc)::value;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const f4 v = ld4(SCl + (J * 4 + t) * 256);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pv[J & 1][4 * t + q] = v[q];
+          }
+        },
+        no_epre,
+        [&](auto Jc, auto ec, const auto&) {
+          constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
+          ho[J][e] = __fmul_rn(__fmul_rn(ho[J][e], pv[J & 1][e]), om);
+        },
+        done, [&](auto Jc) { tile_store(SZl, Jc, ho[decltype(Jc)::value]); }, stp, 16);
+  };
+  bwd(xsm(true, L + 1), xsm(true, L), ic<D>, L);               // W_fᵀ [W][D]
+  R32STAMP(stp, 4);
+  for (int i = L; i >= 2; --i) bwd(xsm(true, i), xsm(true, i - 1), ic<W>, i - 1);
+
+  // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op
+  // sequence; dZ0 is only ever summed (dw0 = Σ dZ0·x, db0 = Σ dZ0), so each
+  // tile's 16 × 2 per-row values are reduce-scattered over the 16 lanes of a
+  // 16-row block (xor 8, 4, 2, 1) and stored as [n_pad/16][2][W] partials:
+  // lane c ends with the sums of registers 2(c & 7), 2(c & 7) + 1 — two
+  // adjacent features — of Σdz·x (c < 8) or Σdz (c >= 8)
+  const int c16 = lane & 15;
+  float* PZ = SZ + (int64_t)blk * 2 * W + (c16 >> 3) * W + 4 * h + 8 * ((c16 >> 1) & 3) +
+              2 * (c16 & 1);
+  gemm32<W, JW, 1, 0, 8, 8>(
+      xsm(true, 1), nullptr, ring, hb, ho, tid, lane, no_pre,
+      [&](auto Jc, u4 (&ep)[8]) {              // w0 (ep[t]) and b0 (ep[4 + t]) of tile J
+        constexpr int J = decltype(Jc)::value;
+        static_for<0, 4>([&](auto tc) {
+          constexpr int t = decltype(tc)::value;
+          ep[t] = ds_read16<(32 * J + 8 * t) * 4>(bias_lane);
+          ep[4 + t] = ds_read16<(W + 32 * J + 8 * t) * 4>(bias_lane);
+        });
+      },
+      [&](auto Jc, auto ec, const auto& ep) {
+        constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
+        const float z = __fadd_rn(__fmul_rn(x, epv(ep, e)), epv(ep + 4, e));
+        float s, co;
+        sincos_fast(__fmul_rn(om, z), &s, &co);
+        ho[J][e] = __fmul_rn(__fmul_rn(ho[J][e], co), om);
+      },
+      done,
+      [&](auto Jc) {
+        constexpr int J = decltype(Jc)::value;
+        float v[32];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          v[e] = __fmul_rn(ho[J][e], x);
+          v[16 + e] = ho[J][e];
+        }
+        const bool b8 = c16 & 8, b4 = c16 & 4, b2 = c16 & 2, b1 = c16 & 1;
+        float w16[16], w8[8], w4[4], w2[2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          w16[i] = (b8 ? v[i + 16] : v[i]) + __shfl_xor(b8 ? v[i] : v[i + 16], 8, 64);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          w8[i] = (b4 ? w16[i + 8] : w16[i]) + __shfl_xor(b4 ? w16[i] : w16[i + 8], 4, 64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          w4[i] = (b2 ? w8[i + 4] : w8[i]) + __shfl_xor(b2 ? w8[i] : w8[i + 4], 2, 64);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          w2[i] = (b1 ? w4[i + 2] : w4[i]) + __shfl_xor(b1 ? w4[i] : w4[i + 2], 1, 64);
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 o2 = {w2[0], w2[1]};
+        __builtin_nontemporal_store(o2, reinterpret_cast<f2*>(PZ + 32 * J));
+      }, stp, 24);
+  R32STAMP(stp, 5);
+}
+
+// ---------------------------------------------------------------------------
 // Parameter-parallel step: weight/bias gradients reduced over all rows, then
 // Adam.  Tiles per fit: L·(W/T)² hidden + (D/TD)(W/T) final + W/64 first.
 //
@@ -1778,7 +2389,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // transposed fp32 copy, both split copies of the weights for the row kernel.
 constexpr int kFx = 24;
 
-template <int TJ, int TK, int NW, int WW, int OD, bool KSX>
+template <int TJ, int TK, int NW, int WW, int OD, int KSX>
 __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
                                            const float* __restrict__ B, int FB, int j0, int k0,
                                            int rb0, int n_blocks, float* G, float* P, float* M,
@@ -1798,8 +2409,8 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   // runtime integer divisions in the Adam epilogue (parameter kernel −0.8 %,
   // 200-epoch sweep +0.5 %, profiles/r02/ab_params_ct_width.log)
   constexpr int W = WW, kOD = OD;
-  // KSX: the split copies go out in the K-split row kernel's layout
-  // (xoff_ks).  Compile-time: a runtime layout select here put the epilogue's
+  // KSX: the layout of the split copies (kLayX / kLayKs / kLay32, the
+  // group's row kernel's).  Compile-time: a runtime layout select here put the epilogue's
   // staging arrays in scratch (576 B/lane) and made the W = 512 parameter
   // kernel 7x slower.
   (void)a;
@@ -1999,7 +2610,7 @@ template <int W, int D, bool X3, bool SMALL = false> struct ParamsCfg {
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
-template <int W, int D, bool X3, bool SMALL = false, bool KSX = false>
+template <int W, int D, bool X3, bool SMALL = false, int KSX = kLayX>
 __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
                                   (ParamsCfg<W, D, X3, SMALL>::MINB))
     k_step_params(KArgs a) {
@@ -2130,14 +2741,14 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   if (i >= fw) {                                       // Wf [D][W] → Wfᵀ [W][D]
     const int64_t r = i - fw;
     if (r < (int64_t)D * W) {
-      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, L + 1, (int)(r / W), (int)(r % W), p);
+      if (XS) put_w(XS, wlayout(a), W, D, L, L + 1, (int)(r / W), (int)(r % W), p);
       else PT[(int64_t)L * W * W + (r % W) * D + r / W] = p;
     }
   } else if (i >= 2 * W) {                             // Wi [W][W] → Wiᵀ
     const int64_t r = (i - 2 * W) % ((int64_t)W * W + W);
     const int64_t layer = (i - 2 * W) / ((int64_t)W * W + W);
     if (r < (int64_t)W * W) {
-      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, (int)layer + 1, (int)(r / W), (int)(r % W), p);
+      if (XS) put_w(XS, wlayout(a), W, D, L, (int)layer + 1, (int)(r / W), (int)(r % W), p);
       else PT[layer * W * W + (r % W) * W + r / W] = p;
     }
   }
@@ -2210,13 +2821,13 @@ __global__ void k_transpose_params(KArgs a) {
       const int64_t k = u / W, j = u % W;  // PT_i[k][j] = W_i[j][k]
       const float p = P[off_hidden_w(W, (int)i + 1) + j * W + k];
       if (PT) PT[e] = p;
-      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, (int)i + 1, (int)j, (int)k, p);
+      if (XS) put_w(XS, wlayout(a), W, D, L, (int)i + 1, (int)j, (int)k, p);
     } else {
       const int64_t u = e - nh;
       const int64_t k = u / D, j = u % D;  // WfT[k][j] = Wf[j][k]
       const float p = P[off_final_w(W, L) + j * W + k];
       if (PT) PT[e] = p;
-      if (XS) put_w(XS, a.rows_ks != 0, W, D, L, L + 1, (int)j, (int)k, p);
+      if (XS) put_w(XS, wlayout(a), W, D, L, L + 1, (int)j, (int)k, p);
     }
   }
 }
@@ -2369,6 +2980,19 @@ bool rows_ks_for(const nerfhip_group* g, const nerfhip_sizes& s) {
   return (int64_t)g->n_fits * (s.n_pad / kRowPad) <= kKsMaxWorkgroups;
 }
 
+// The 32-row kernel (k_step_rows32) for bf16x3 groups with W = 256, D = 128
+// whose rows fill whole 128-row workgroups, unless the group takes the
+// K-split kernel.  Opt-in while it is slower than the 16-row kernel
+// (NERFHIP_ROWS32 = 1; kRows32Default).
+constexpr bool kRows32Default = false;
+bool rows32_for(const nerfhip_group* g, const nerfhip_sizes& s, bool ks) {
+  if (ks || g->precision != NERFHIP_PRECISION_BF16X3 || g->W != 256 || g->D != 128 ||
+      s.n_pad % 128 != 0)
+    return false;
+  const char* e = getenv("NERFHIP_ROWS32");
+  return e ? e[0] == '1' : kRows32Default;
+}
+
 KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   KArgs a{};
   a.W = g->W; a.D = g->D; a.N = g->N; a.n_pad = (int32_t)s.n_pad;
@@ -2391,6 +3015,7 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   a.ws_stride = s.wsplit;
   a.wsplit = static_cast<uint16_t*>(g->wsplit);
   a.rows_ks = rows_ks_for(g, s) ? 1 : 0;
+  a.rows32 = rows32_for(g, s, a.rows_ks != 0) ? 1 : 0;
   // NERFHIP_ROWS_LDS_PAD / NERFHIP_PARAMS_LDS_PAD: dynamic LDS per workgroup
   // of the regular row / parameter kernels, KB (schedule experiments)
   if (const char* e = getenv("NERFHIP_ROWS_LDS_PAD")) a.rows_dyn_lds = 1024u * (uint32_t)atoi(e);
@@ -2438,6 +3063,9 @@ int launch_rows(const KArgs& a, hipStream_t st) {
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
+  if constexpr (X3 && W == 256 && D == 128) {
+    if (a.rows32) return launch_rows32<W, D>(a, st);   // its own translation unit (NERFHIP_KIND 3)
+  }
   const int grid = grid_for(a.n_fits, a.n_pad / RowsCfg<W>::ROWS);
   if (a.mode == 0)
     hipLaunchKernelGGL((k_step_rows<W, D, X3, true>), dim3(grid), dim3(RowsCfg<W>::THREADS),
@@ -2478,8 +3106,15 @@ int launch_params(const KArgs& a, hipStream_t st) {
   // kernel runs: bf16x3, W >= 128, D = 128 — rows_ks_for)
   if constexpr (X3 && W >= 128 && D == 128) {
     if (a.rows_ks && a.n_split == 1) {   // fused epilogue writes the K-split layout
-      hipLaunchKernelGGL((k_step_params<W, D, X3, false, true>), dim3(grid),
+      hipLaunchKernelGGL((k_step_params<W, D, X3, false, kLayKs>), dim3(grid),
                          dim3(ParamsCfg<W, D, X3>::THREADS), 0, st, a);
+      return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+    }
+  }
+  if constexpr (X3 && W == 256 && D == 128) {
+    if (a.rows32 && a.n_split == 1) {    // ... or the 32-row kernel's
+      hipLaunchKernelGGL((k_step_params<W, D, X3, false, kLay32>), dim3(grid),
+                         dim3(ParamsCfg<W, D, X3>::THREADS), a.params_dyn_lds, st, a);
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
@@ -2489,12 +3124,33 @@ int launch_params(const KArgs& a, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
+// The 32-row kernel is compiled only in its own translation unit
+// (NERFHIP_KIND 3: -amdgpu-mfma-vgpr-form, accumulators in VGPRs, the B
+// operand in AGPRs); every other unit sees the declaration only.
+#if NERFHIP_KIND == 3 || NERFHIP_PART < 0
+template <int W, int D>
+int launch_rows32(const KArgs& a, hipStream_t st) {
+  const int grid = grid_for(a.n_fits, a.n_pad / 128);
+  if (a.mode == 0)
+    hipLaunchKernelGGL((k_step_rows32<W, D, true>), dim3(grid), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_step_rows32<W, D, false>), dim3(grid), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+}
+#endif
+
 // NERFHIP_KIND splits a part further: 1 = row kernels only, 2 = parameter
-// kernels only (compiled with different flags, nerf_attention/_build.py), 0 = both
+// kernels only (compiled with different flags, nerf_attention/_build.py),
+// 3 = the 32-row kernel only, 0 = all
 #ifndef NERFHIP_KIND
 #define NERFHIP_KIND 0
 #endif
-#if NERFHIP_KIND == 1
+#if NERFHIP_KIND == 3
+#define NERFHIP_INST_ONE(W, D, X)
+#if NERFHIP_PART == 6
+template int launch_rows32<256, 128>(const KArgs&, hipStream_t);
+#endif
+#elif NERFHIP_KIND == 1
 #define NERFHIP_INST_ONE(W, D, X) template int launch_rows<W, D, X>(const KArgs&, hipStream_t);
 #elif NERFHIP_KIND == 2
 #define NERFHIP_INST_ONE(W, D, X) template int launch_params<W, D, X>(const KArgs&, hipStream_t);
@@ -2574,6 +3230,31 @@ int row_metrics(const KArgs& a, const float* ybuf, int64_t ystride, float* rc, f
 extern "C" {
 
 int nerfhip_abi_version(void) { return NERFHIP_ABI_VERSION; }
+
+// Diagnostic compile-time switches (nerfhip.h NERFHIP_BUILD_*).  Every
+// NERFHIP_EXP_* / NERFHIP_DIAG_* name the source tests must be listed here
+// (tests/test_capi.py checks the source against this list); variant builds
+// (tools/build_variant.py) pass them to every translation unit, this one too.
+int nerfhip_build_flags(void) {
+  int f = 0;
+#if defined(NERFHIP_EXP_ADAM_NO_SPLIT_COPIES) || defined(NERFHIP_EXP_DWORD_STORES) ||       \
+    defined(NERFHIP_EXP_KS_ALTFIT) || defined(NERFHIP_EXP_KS_LINEAR) ||                      \
+    defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
+    defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
+    defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
+    defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
+    defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \
+    (NERFHIP_SINCOS != 0)
+  f |= NERFHIP_BUILD_EXP;
+#endif
+#ifdef NERFHIP_STAMPS
+  f |= NERFHIP_BUILD_STAMPS;
+#endif
+#if defined(NERFHIP_DIAG_ROWS_TWICE)
+  f |= NERFHIP_BUILD_DIAG;
+#endif
+  return f;
+}
 
 #ifdef NERFHIP_STAMPS
 // diagnostic build only: device buffer of [blocks][4 waves][8] u64 stamps
@@ -2828,8 +3509,9 @@ int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out) {
   nerfhip_sizes s;
   fill_sizes(g->W, g->D, g->N, g->L_max, g->epochs, &s);
   const KArgs a = make_args(g, s);
-  const int rows_per_wg = a.rows_ks ? 16 : 64;
-  out->rows_variant = a.rows_ks ? NERFHIP_ROWS_KSPLIT : NERFHIP_ROWS_REGULAR;
+  const int rows_per_wg = a.rows_ks ? 16 : a.rows32 ? 128 : 64;
+  out->rows_variant = a.rows_ks ? NERFHIP_ROWS_KSPLIT
+                                : a.rows32 ? NERFHIP_ROWS_32 : NERFHIP_ROWS_REGULAR;
   out->grad_split = a.n_split;
   out->rows_workgroups = grid_for(a.n_fits, (int)(s.n_pad / rows_per_wg));
   out->params_workgroups =

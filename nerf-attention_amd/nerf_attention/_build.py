@@ -45,6 +45,12 @@ N_PARTS = 9   # NERFHIP_PART 0 = host ABI + small kernels, 1..8 = (W, precision)
 # the W = 256 row kernel measured ~2 % slower — so only the parameter side
 # drops SLP.
 KIND_FLAGS = {1: [], 2: ["-fno-slp-vectorize"]}
+# NERFHIP_KIND 3: the 32-row kernel (k_step_rows32), part 6 (W = 256, bf16x3)
+# only.  Its MFMAs take the B operand from accumulator registers and keep the
+# accumulators in VGPRs; -amdgpu-mfma-vgpr-form makes the compiler select the
+# VGPR form of the MFMA destination (without it the accumulators go to AGPRs
+# too, and 192 AGPRs of B plus 32 of accumulators do not fit beside them).
+R32_UNITS = [(6, 3, ["-mllvm", "-amdgpu-mfma-vgpr-form=1"])]
 
 
 def build(force: bool = False, verbose: bool = True) -> Path:
@@ -59,10 +65,11 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function", "-I", str(INCLUDE)]
     objs, procs = [], []
-    units = [(0, 0)] + [(part, kind) for part in range(1, N_PARTS) for kind in KIND_FLAGS]
-    for part, kind in units:
+    units = ([(0, 0, [])] + [(part, kind, KIND_FLAGS[kind]) for part in range(1, N_PARTS)
+                             for kind in KIND_FLAGS] + R32_UNITS)
+    for part, kind, flags in units:
         obj = obj_dir / (f"nerfhip_p{part}.o" if kind == 0 else f"nerfhip_p{part}k{kind}.o")
-        cmd = base + KIND_FLAGS.get(kind, []) + [f"-DNERFHIP_PART={part}",
+        cmd = base + flags + [f"-DNERFHIP_PART={part}",
                                                  f"-DNERFHIP_KIND={kind}", "-c", str(SOURCES[0]),
                                                  "-o", str(obj)]
         if verbose:

@@ -18,7 +18,7 @@ import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 from ._build import LIB
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # nerfhip_precision (include/nerfhip.h)
 PRECISIONS = {"fp32": 0, "bf16x3": 1}
@@ -80,7 +80,7 @@ class NerfhipPlan(ctypes.Structure):
                                         "params_workgroups", "launches_per_epoch", "reserved")]
 
 
-ROWS_VARIANTS = {0: "regular", 1: "ksplit"}   # nerfhip_rows_variant
+ROWS_VARIANTS = {0: "regular", 1: "ksplit", 2: "rows32"}   # nerfhip_rows_variant
 
 # every symbol include/nerfhip.h declares, with its ctypes signature
 SIGNATURES = {
@@ -93,6 +93,7 @@ SIGNATURES = {
                                           POINTER(NerfhipTiming)]),
     "nerfhip_siren_forward": (c_int32, [POINTER(NerfhipGroup), c_void_p]),
     "nerfhip_group_plan": (c_int32, [POINTER(NerfhipGroup), POINTER(NerfhipPlan)]),
+    "nerfhip_build_flags": (c_int32, []),
     "nerfhip_svd_rank_metrics": (c_int32, [POINTER(NerfhipSvdBatch), c_void_p]),
     "nerfhip_kv_analysis": (c_int32, [POINTER(NerfhipKvAnalysisBatch), c_void_p]),
     "nerfhip_rng_uniform_segments": (c_int32, [c_void_p, POINTER(c_int32), POINTER(ctypes.c_uint32),

@@ -110,19 +110,23 @@ def pool_job_fork(shape: tuple, tt: np.ndarray, jobs: list, num_layers: int,
     return len(jobs)
 
 
-def pool_job(shm_name: str, shape: tuple, tt: np.ndarray, jobs: list, num_layers: int,
+def pool_job(path: str, shape: tuple, tt: np.ndarray, jobs: list, num_layers: int,
              num_kv_heads: int) -> int:
     """Worker: fill slots [k] of the shared [n, 2, seq_len, head_dim] float32
-    buffer with slice (layer, head) for every (k, layer, head) in jobs."""
-    from multiprocessing import shared_memory
-    shm = shared_memory.SharedMemory(name=shm_name)    # the parent unlinks it
-    try:
-        buf = np.ndarray(shape, dtype=np.float32, buffer=shm.buf)
-        for k, layer, head in jobs:
-            slice_np(tt, layer, head, num_layers, num_kv_heads, shape[3], buf[k, 0], buf[k, 1])
-        del buf
-    finally:
-        shm.close()
+    file mapping at `path` (the parent removes it) with slice (layer, head)
+    for every (k, layer, head) in jobs."""
+    buf = np.memmap(path, dtype=np.float32, mode="r+", shape=shape)
+    for k, layer, head in jobs:
+        slice_np(tt, layer, head, num_layers, num_kv_heads, shape[3], buf[k, 0], buf[k, 1])
+    buf.flush()
+    del buf
     return len(jobs)
 
 
+if __name__ == "__main__":   # a worker process of synthetic.kv_slices (spawn path)
+    import json
+    import sys
+    with open(sys.argv[1]) as f:
+        job = json.load(f)
+    pool_job(job["path"], tuple(job["shape"]), np.asarray(job["tt"], dtype=np.float32),
+             [tuple(j) for j in job["jobs"]], job["num_layers"], job["num_kv_heads"])

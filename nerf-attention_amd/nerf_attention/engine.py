@@ -536,8 +536,8 @@ class StreamingJob:
     all of them.  Here the group plan is fixed up front from each fit's
     (config, seq_len, d_head) — `plan_groups` needs nothing else — and
     `add(i, spec)` hands over fit i's target and init: the moment the last
-    member of a group (a chunk of consecutive reference-order fits of one
-    width) arrives, a launcher thread of that group packs and uploads its
+    member of a group (a chunk of same-width fits, plan_groups) arrives, a
+    launcher thread of that group packs and uploads its
     buffers and enqueues its whole training on its own stream (that call
     blocks on the stream's queue depth for most of the run), while the
     caller goes on drawing the next inits.

@@ -22,7 +22,7 @@ from pathlib import Path
 import numpy as np
 import torch
 
-from ._synth_core import pool_job, slice_np
+from ._synth_core import slice_np
 from .types import KVMetadata
 
 
@@ -93,21 +93,41 @@ def kv_slices(pairs, seq_len: int = 2048, num_layers: int = 32, num_kv_heads: in
             _synth_core._SHARED = None
         out = torch.from_numpy(np.frombuffer(mm, dtype=np.float32).reshape(shape))
     else:
-        # this process has HIP state: fresh interpreters and a named segment
-        from multiprocessing import shared_memory
-        shm = shared_memory.SharedMemory(create=True, size=nbytes)
+        # this process has HIP state: fresh interpreters — plain child
+        # processes running _synth_core.py as a script (numpy only), not a
+        # multiprocessing spawn pool, whose start method launches a resource
+        # tracker process that outlives the caller (the process BENCH_r04
+        # found left at the end) — writing into a memory-mapped file under
+        # /dev/shm
+        import subprocess
+        import sys
+        import tempfile
+        shm_dir = "/dev/shm" if os.path.isdir("/dev/shm") else None
+        fd, path = tempfile.mkstemp(prefix="nerf_synth_", dir=shm_dir)
+        specs = []
         try:
-            with ProcessPoolExecutor(max_workers=workers,
-                                     mp_context=mp.get_context("spawn")) as ex:
-                for f in [ex.submit(pool_job, shm.name, shape, tt, part, num_layers,
-                                    num_kv_heads) for part in parts]:
-                    f.result()
-            buf = np.ndarray(shape, dtype=np.float32, buffer=shm.buf)
-            out = torch.from_numpy(buf.copy())
+            os.ftruncate(fd, nbytes)
+            procs = []
+            for w, part in enumerate(parts):
+                spec = f"{path}.job{w}.json"
+                specs.append(spec)
+                with open(spec, "w") as f:
+                    json.dump({"path": path, "shape": list(shape), "tt": tt.tolist(),
+                               "jobs": part, "num_layers": num_layers,
+                               "num_kv_heads": num_kv_heads}, f)
+                procs.append(subprocess.Popen([sys.executable, _synth_core.__file__, spec]))
+            bad = [p.args for p in procs if p.wait() != 0]
+            if bad:
+                raise RuntimeError(f"synthetic KV worker failed: {bad[0]}")
+            buf = np.memmap(path, dtype=np.float32, mode="r", shape=shape)
+            out = torch.from_numpy(np.array(buf))
             del buf
         finally:
-            shm.close()
-            shm.unlink()
+            os.close(fd)
+            os.unlink(path)
+            for spec in specs:
+                if os.path.exists(spec):
+                    os.unlink(spec)
     return [(out[k, 0], out[k, 1]) for k in range(len(pairs))]
 
 

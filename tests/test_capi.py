@@ -11,7 +11,8 @@ import pytest
 
 from nerf_attention import _build, _native
 
-HEADER = Path(__file__).resolve().parent.parent / "include" / "nerfhip.h"
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "nerfhip.h"
 
 
 @pytest.fixture(scope="module")
@@ -99,13 +100,14 @@ def _plan(lib, **kw):
     return rc, p
 
 
-def test_group_plan(lib):
+def test_group_plan(lib, monkeypatch):
     """nerfhip_group_plan (host only): BASELINE config 2, one medium fit at
     seq 2048 in bf16x3 with the split-K workspace, takes the K-split row kernel
     (one 16-row block per workgroup) and 8 gradient row slices on 64 x 64
     tiles; a wide fit at 8192 (128 regular workgroups) K-split rows too and
-    128 x 128 tiles x 8 slices; a 40-fit
-    sweep chunk the regular kernels, fused."""
+    128 x 128 tiles x 8 slices; a 40-fit W = 256
+    sweep chunk the 32-row kernel (128-row workgroups), fused; a 40-fit
+    W = 512 chunk the regular kernels."""
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=1,
                   grad_partial=1)
     assert rc == 0
@@ -116,9 +118,18 @@ def test_group_plan(lib):
                   grad_partial=1)
     assert rc == 0 and (p.rows_variant, p.grad_split) == (1, 8)       # 128 regular -> K-split
     assert p.params_workgroups == 8 * (3 * 16 + 1 * 4 + 512 // 64)     # 60 128x128 tiles
+    monkeypatch.setenv("NERFHIP_ROWS32", "1")
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=40, L_max=3, epochs=2000, precision=1)
+    assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (2, 1, 2)
+    assert p.rows_workgroups == 8 * 16 * 5                            # XCD map: 40 fits x 16
+    rc, p = _plan(lib, W=512, D=128, N=2048, n_fits=40, L_max=2, epochs=2000, precision=1)
     assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (0, 1, 2)
     assert p.rows_workgroups == 8 * 32 * 5                            # XCD map: 40 fits x 32
+    # 32-row kernel only where 128-row workgroups tile the rows (n_pad % 128)
+    rc, p = _plan(lib, W=256, D=128, N=1984, n_fits=40, L_max=2, epochs=2000, precision=1)
+    assert rc == 0 and p.rows_variant == 0                            # n_pad 1984 = 15.5 x 128
+    rc, p = _plan(lib, W=256, D=64, N=2048, n_fits=40, L_max=2, epochs=2000, precision=1)
+    assert rc == 0 and p.rows_variant == 0                            # D = 64: regular
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=0)
     assert rc == 0 and p.rows_variant == 0                            # fp32: regular rows
     # five wide fits at 512 without the workspace (the engine gives none to
@@ -128,6 +139,20 @@ def test_group_plan(lib):
     assert p.rows_workgroups == 5 * 512 // 16
     assert _plan(lib, W=100, D=128, N=64, n_fits=1, L_max=1, epochs=1)[0] == -1
     assert lib.nerfhip_group_plan(None, None) == -5
+
+
+def test_shipped_library_is_a_product_build(lib):
+    """The in-tree libnerfhip.so reports no diagnostic compile-time switch
+    (nerfhip_build_flags: NERFHIP_EXP_* timing builds may compute wrong
+    results on purpose, NERFHIP_STAMPS / NERFHIP_DIAG_* alter the kernels),
+    and every such macro the engine source tests is one the function checks."""
+    assert lib.nerfhip_build_flags() == 0
+    src = (ROOT / "nerf-attention_amd" / "csrc" / "nerfhip.hip").read_text()
+    body = src[src.index("int nerfhip_build_flags(void)"):]
+    body = body[:body.index("\n}\n")]
+    names = set(re.findall(r"\b(NERFHIP_(?:EXP|DIAG)_[A-Z0-9_]+)\b", src))
+    missing = sorted(n for n in names if n not in body)
+    assert not missing, missing
 
 
 def _mt_seed(seed):

@@ -419,3 +419,26 @@ def test_streaming_job_launch_error_surfaces(monkeypatch):
         job.add(i, p)
     with pytest.raises(engine._native.NerfhipError):
         list(job.finished())
+
+
+def test_synthetic_spawn_pool_bitwise_and_leaves_nothing(monkeypatch):
+    """The generator's spawn-process path (taken once the process holds HIP
+    state) gives the same bits as one process, and leaves no child process
+    (no multiprocessing resource tracker: BENCH_r04 procs_at_end) and no
+    /dev/shm file behind."""
+    import glob
+    import multiprocessing as mp
+    from nerf_attention import synthetic
+    monkeypatch.setattr(synthetic, "_hip_untouched", lambda: False)
+    monkeypatch.setattr(synthetic, "POOL_MIN_ROWS", 0)
+    monkeypatch.setattr(synthetic, "_threads", lambda: 2)
+    pairs = [(0, 0), (3, 1), (5, 2)]
+    before = set(glob.glob("/dev/shm/nerf_synth_*"))
+    got = synthetic.kv_slices(pairs, seq_len=256, num_layers=8, num_kv_heads=4)
+    for (l, h), (k, v) in zip(pairs, got):
+        k0, v0 = kv_slice(l, h, seq_len=256, num_layers=8, num_kv_heads=4)
+        assert torch.equal(k, k0) and torch.equal(v, v0)
+    assert mp.active_children() == []
+    assert set(glob.glob("/dev/shm/nerf_synth_*")) == before
+    from multiprocessing import resource_tracker
+    assert getattr(resource_tracker._resource_tracker, "_pid", None) is None

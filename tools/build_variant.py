@@ -29,12 +29,13 @@ def main():
     base = [_build.HIPCC, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC",
             "-Wno-unused-function", "-I", str(_build.INCLUDE), *rest]
     objs, procs = [], []
-    units = [(0, 0)] + [(p, k) for p in range(1, _build.N_PARTS) for k in _build.KIND_FLAGS]
-    for part, kind in units:
+    units = ([(0, 0, [])] + [(p, k, _build.KIND_FLAGS[k]) for p in range(1, _build.N_PARTS)
+                             for k in _build.KIND_FLAGS] + _build.R32_UNITS)
+    for part, kind, flags in units:
         fname = f"nerfhip_p{part}.o" if kind == 0 else f"nerfhip_p{part}k{kind}.o"
         if part in parts:
             obj = odir / fname
-            procs.append(subprocess.Popen(base + _build.KIND_FLAGS.get(kind, []) + [
+            procs.append(subprocess.Popen(base + flags + [
                 f"-DNERFHIP_PART={part}", f"-DNERFHIP_KIND={kind}", "-c",
                 str(_build.SOURCES[0]), "-o", str(obj)]))
         else:
