@@ -39,6 +39,7 @@ Also reported (rank 0):
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -51,9 +52,12 @@ sys.path.insert(0, str(ROOT / "nerf-attention_amd"))
 # one hardware queue per width-group stream (the engine runs ~7 streams per
 # GPU; HIP's default of 4 queues makes some of them share a queue, in order:
 # the 2000-epoch sweep measured 27.0 fits/s with 4, 27.7 with 8 on one box,
-# profiles/r04/queues_ab.log).  The GPU boxes export HIP's default (4), so it
-# is raised, not defaulted.  Must be set before the HIP runtime initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+# profiles/r04/queues_ab.log).  The GPU boxes export HIP's default (4), so an
+# unset value or HIP's default is raised to 8; any other explicit value wins,
+# and NERFHIP_KEEP_HW_QUEUES=1 keeps even the default (4-vs-8 A/B).  Must be
+# set before the HIP runtime initialises.
+if (os.environ.get("NERFHIP_KEEP_HW_QUEUES") != "1"
+        and os.environ.get("GPU_MAX_HW_QUEUES", "").strip() in ("", "4")):
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np
@@ -239,6 +243,14 @@ ISO_EPOCHS = 101   # isolated leg: 25 timed launches (every 4th epoch from epoch
 # rocprofv3 --kernel-trace --stats, and its PMC passes)
 ISO_PROFILE = "profiles/r04/rocprof_kernel_stats_isolated_rows256.csv"
 ISO_PMC = ROOT / "profiles" / "r04" / "pmc_isolated_rows256.json"
+
+
+def lib_sha16() -> str:
+    """First 16 hex digits of the engine library's SHA-256: a committed PMC
+    summary names the library it measured, and its bytes / MFMA-busy figures
+    are reported only for that same library."""
+    from nerf_attention import _build
+    return hashlib.sha256(Path(os.environ.get("NERFHIP_LIB", _build.LIB)).read_bytes()).hexdigest()[:16]
 
 
 def heaviest_group(specs, width: int, device: int = 0) -> list:
@@ -464,8 +476,14 @@ def main() -> None:
             iso_pmc = None
             if ISO_PMC.exists():
                 iso_pmc = json.loads(ISO_PMC.read_text()).get(f"{kname}[{args.precision}]")
-            iso_bytes = iso_pmc and iso_pmc["bytes"]
+            pmc_lib = iso_pmc and iso_pmc.get("lib_sha16")
+            cur_lib = lib_sha16()
+            if iso_pmc and pmc_lib != cur_lib:
+                # the committed counters describe another build of the kernel
+                iso_pmc = {"stale": True, "pmc_lib_sha16": pmc_lib, "lib_sha16": cur_lib}
+            iso_bytes = iso_pmc and iso_pmc.get("bytes")
             hbm_iso = iso_bytes and iso_bytes / (iso["avg_launch_ms"] * 1e-3) / 1e9
+            alg_bytes = sum(4 * N * 128 + 24 * c.num_parameters(128) for c in gcf)
             roof = {"bound": "mfma", "achieved": iso["achieved"],
                     "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": iso["frac"],
@@ -484,6 +502,11 @@ def main() -> None:
                                       "same isolated group (tools/r4/iso_prof.sh, "
                                       "profiles/r04/pmc_isolated_rows256.json)",
                     "mfma_busy": iso_pmc and iso_pmc.get("mfma_busy"),
+                    "algorithmic_bytes": alg_bytes,
+                    "algorithmic_bytes_kind": "SURVEY.md §8d per fit-epoch 4·N·D target + 24·P "
+                                              "params/Adam read+write, x fits of the group "
+                                              "(activations assumed on-chip)",
+                    "traffic_over_algorithmic": iso_bytes and round(iso_bytes / alg_bytes, 2),
                     "mfma_busy_kind": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GPU-active "
                                       "cycles), rocprofv3 PMC pass of the same isolated group",
                     "hbm_gbs": hbm_iso and round(hbm_iso, 1),

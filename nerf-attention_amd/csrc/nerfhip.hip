@@ -138,10 +138,12 @@ __device__ unsigned long long* g_stamps = nullptr;
 // the 32-row kernel's stamps: [blocks][4 waves][32] from a.pstamps + 262144
 // (after the parameter and K-split kernels' regions), through a pointer the
 // kernel hands to its phases (g_stamps is per translation unit)
-#define R32STAMP_ADD(p, k, v)                                                          \
-  do {                                                                                 \
-    if ((p) && (threadIdx.x & 63) == 0)                                                \
-      (p)[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + (k)] += (v);            \
+// R32STAMP_ADD accumulates in registers (a read-modify-write of global
+// memory would wait for every vector-memory op in flight and distort exactly
+// the waits it measures); the kernel stores the sums at its end
+#define R32STAMP_ADD(acc, k, v) \
+  do {                          \
+    (acc)[(k)] += (v);          \
   } while (0)
 #define R32STAMP(p, k)                                                                 \
   do {                                                                                 \
@@ -162,8 +164,8 @@ __device__ unsigned long long* g_stamps = nullptr;
           __builtin_amdgcn_s_memrealtime();                                            \
   } while (0)
 #else
-#define R32STAMP_ADD(p, k, v) \
-  do {                        \
+#define R32STAMP_ADD(acc, k, v) \
+  do {                          \
   } while (0)
 #define R32STAMP(p, k) \
   do {                 \
@@ -1687,13 +1689,20 @@ struct R32Dma {
       : rsrc(__builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7fffffff, 0x00020000)),
         voff(2 * ((tid >> 4) * KC + 8 * ((tid & 15) ^ (tid >> 4)))),
         wave(__builtin_amdgcn_readfirstlane(tid >> 6)) {}
+  // The whole source offset goes into the per-lane VGPR (an asm add the
+  // backend cannot split): as an SGPR soffset, hipcc materialised each
+  // constant into an SGPR right before its load and rewrote that SGPR one
+  // instruction later — the pattern behind the K-split co-residency fault
+  // (KsPhase).
   template <int U> __device__ __forceinline__ void issue(uint16_t* ring) const {
     typedef __attribute__((address_space(3))) void lds_void;
     uint16_t* buf = ring + (U % NR32) * CH;
     static_for<0, NDMA>([&](auto mc) {
       constexpr int m = decltype(mc)::value;
+      int v;
+      asm("v_add_u32 %0, %1, %2" : "=v"(v) : "i"(2 * U * CH + 32 * m * KC), "v"(voff));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(buf + 8 * (256 * m + 64 * wave)),
-                                               16, voff, 2 * U * CH + 32 * m * KC, 0, 0);
+                                               16, v, 0, 0, 0);
     });
   }
 };
@@ -1720,9 +1729,13 @@ __device__ __forceinline__ void r32_prefetch(const uint16_t* src, uint16_t* ring
 //   elem(J, e, ep)  epilogue of element e of tile J, spread over tile J+1's
 //               k-steps (16 / (KT·NH) per k-step);
 //   done(J, hi, lo)  hands over tile J's accumulators at its end;
-//   flush(J)    tile J's stores, at the top of tile J+2.
-// NST / NLD: the exact store / load instruction counts of flush / pre (or
-// fewer: fewer only over-waits), as in gemm_phase_x3.
+//   flush(J, t) tile J's stores of register group t (0..3), in k-step t of
+//               tile J+2 (after that sub-chunk's DMA): spread over the
+//               k-steps, a 16-B store's issue stall sits beside MFMAs
+//               instead of in a burst ahead of them (≈870 cycles per tile
+//               as a burst, profiles/r05/stamps32b_*.log).
+// NST / NLD: the exact store / load instruction counts of a whole flush(J) /
+// pre (or fewer: fewer only over-waits).
 // Phase boundaries.  The phase's first NR32 - 1 sub-chunks were issued before
 // it (r32_prefetch), followed by NAFTER vector-memory ops (the previous
 // phase's last two flushes, or layer 0's stores; fewer only over-waits), and
@@ -1740,14 +1753,15 @@ __device__ __forceinline__ void r32_prefetch(const uint16_t* src, uint16_t* ring
 // of tile 0 on.  Split between the phases instead, ≈1,100 VALU per phase
 // (128 elements and 192 accumulator-register writes) ran with nothing to
 // overlap at one wave per SIMD.
-template <int K, int JT, int NST, int NLD, int NEP, int NAFTER, int NB, int NTS, class Pre,
-          class Epre, class Elem, class Done, class Flush>
+template <int K, int JT, int NST, int NLD, int NEP, int NAFTER, int SSLOT, int NB, int NTS,
+          class Pre, class Epre, class Elem, class Done, class Flush>
 __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
                                        const uint16_t* __restrict__ next, uint16_t* ring,
                                        S8 (&b)[NB], const float (&hs)[NTS][16], int tid,
                                        int lane, Pre&& pre, Epre&& epre, Elem&& elem,
                                        Done&& done, Flush&& flush,
-                                       unsigned long long* stp = nullptr, int sslot = 8) {
+                                       unsigned long long (&sacc)[32]) {
+  constexpr int sslot = SSLOT;
   using C = R32Cfg<K>;
   constexpr int NH = C::NH, KT = C::KT, U = JT * NH, CH = C::CH, PLB = C::PLB;
   constexpr int NDMA = C::NDMA, EPK = 16 / (KT * NH);
@@ -1799,17 +1813,22 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
     __builtin_amdgcn_sched_barrier(0);
   };
   // vector-memory ops issued after sub-chunk d's DMA and before the wait for
-  // it at the end of iteration d - 1 (d = 0: the phase's first wait), in the
-  // issue order [prefetch DMA 0 .. NR32-2][NAFTER][iteration 0: flush, pre,
-  // DMA(NR32-1)][iteration 1] ...
-  auto younger = [](int d, int upto) {   // ops issued after DMA(d), up to iteration `upto`
-    int n = 0;
-    if (d < NR32 - 1) n += (NR32 - 2 - d) * NDMA + NAFTER;   // rest of the prefetch, NAFTER
-    const int v0 = d < NR32 - 1 ? 0 : d - NR32 + 2;          // iterations after DMA(d)'s own
-    for (int v = v0; v <= upto; ++v) {
-      if (v % NH == 0) n += NLD + (v / NH >= 2 ? NST : 0);
-      if (v + NR32 - 1 < U && v + NR32 - 1 != d) n += NDMA;
+  // it at the end of iteration `upto` (d = 0, upto = -1: the phase's first
+  // wait), in the issue order [prefetch DMA 0 .. NR32-2][NAFTER]
+  // [iteration 0: pre, DMA(NR32-1), flush][iteration 1] ...
+  auto younger = [](int d, int upto) {
+    auto loads = [](int v) { return v % NH == 0 ? NLD : 0; };
+    auto stores = [](int v) { return v % NH == 0 && v / NH >= 2 ? NST : 0; };
+    auto dmas = [](int v) { return v + NR32 - 1 < U ? NDMA : 0; };
+    int n = 0, v0 = 0;
+    if (d < NR32 - 1) {
+      n += (NR32 - 2 - d) * NDMA + NAFTER;   // the rest of the prefetch, NAFTER
+    } else {
+      const int vd = d - NR32 + 1;           // the iteration that issued DMA(d)
+      if (vd <= upto) n += stores(vd);       // its flush comes after the DMA
+      v0 = vd + 1;
     }
+    for (int v = v0; v <= upto; ++v) n += loads(v) + dmas(v) + stores(v);
     return n;
   };
   const unsigned long long t_p0 = MEMTIME();
@@ -1819,8 +1838,8 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
   S8 a_cur = aread(ic<0>, ic<0>);
   lgkm_wait(a_cur);
 #ifdef NERFHIP_STAMPS
-  R32STAMP_ADD(stp, 29, t_p1 - t_p0);          // phase heads: wait for sub-chunk 0
-  R32STAMP_ADD(stp, 30, MEMTIME() - t_p1);     // phase heads: first split + fragment
+  R32STAMP_ADD(sacc, 29, t_p1 - t_p0);          // phase heads: wait for sub-chunk 0
+  R32STAMP_ADD(sacc, 30, MEMTIME() - t_p1);     // phase heads: first split + fragment
 #else
   (void)t_p0; (void)t_p1;
 #endif
@@ -1830,7 +1849,6 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
     constexpr int J = u / NH, hh = u % NH;
     const unsigned long long t_f0 = MEMTIME();
     if constexpr (hh == 0) {
-      if constexpr (J >= 2) flush(ic<J - 2>);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         hi[e] = 0.f;
@@ -1838,7 +1856,7 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
       }
       pre(ic<J>);
     }
-    __builtin_amdgcn_sched_barrier(0);   // flush / pre before the DMA: vmcnt counts in order
+    __builtin_amdgcn_sched_barrier(0);   // pre before the DMA, flush after it: vmcnt counts in order
     const unsigned long long t_d0 = MEMTIME();
     if constexpr (u + NR32 - 1 < U) dm.template issue<u + NR32 - 1>(ring);
     __builtin_amdgcn_sched_barrier(0);
@@ -1847,13 +1865,37 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
       constexpr int kt = decltype(ktc)::value;
       S8 a_nxt = a_cur;
       if constexpr (kt + 1 < KT) a_nxt = aread(uc, ic<kt + 1>);
+      // the next fragment's reads stay ahead of this k-step's MFMAs (left
+      // free, the scheduler sank them below two MFMAs, and their LDS latency
+      // showed at the k-step's closing wait)
+      __builtin_amdgcn_sched_barrier(0);
       if constexpr (J == 0 && hh * KT + kt + 1 < KS) split_b(ic<hh * KT + kt + 1>);
+      if constexpr (hh == 0 && J >= 2 && kt < 4) flush(ic<J - 2>, ic<kt>);
       mfma32x3(a_cur, b[hh * KT + kt], hi, lo);
       if constexpr (J > 0) {
         static_for<0, EPK>([&](auto ec) {
           elem(ic<J - 1>, ic<(hh * KT + kt) * EPK + decltype(ec)::value>, ep);
         });
       }
+#ifndef NERFHIP_R32_VPG
+#define NERFHIP_R32_VPG 6
+#endif
+      // one MFMA, then up to VPG vector ALU instructions, six times: at one
+      // wave per SIMD nothing else fills an MFMA's shadow (it holds the
+      // SIMD's vector issue for 8 of its 32 cycles: ~6 four-cycle VALU fit
+      // beside it), and the free schedule clustered the epilogue VALU after
+      // the MFMAs, where every instruction cost its full issue time
+      if constexpr (NERFHIP_R32_VPG > 0) {
+        static_for<0, 6>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, NERFHIP_R32_VPG, 0);
+        });
+      }
+      // keep the MFMAs (and the epilogue VALU) ahead of the wait for the next
+      // fragment: left free, the scheduler sank five of the six MFMAs below
+      // it and the LDS latency showed in every k-step (at one wave per SIMD
+      // nothing else covers it; gemm_phase_x3's PIN)
+      __builtin_amdgcn_sched_barrier(0);
       if constexpr (kt + 1 < KT) lgkm_wait(a_nxt);
       __builtin_amdgcn_sched_barrier(0);
       a_cur = a_nxt;
@@ -1865,13 +1907,13 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
     vm_wait_barrier(std::integral_constant<int, (u + 1 < U ? younger(u + 1, u) : -1)>{});
 #ifdef NERFHIP_STAMPS
     const unsigned long long t_w1 = MEMTIME();
-    R32STAMP_ADD(stp, sslot, t_d1 - t_d0);      // DMA issue
-    R32STAMP_ADD(stp, sslot + 1, t_w0 - t_d1);  // k-steps (MFMA + epilogue VALU + LDS reads + split)
-    R32STAMP_ADD(stp, sslot + 2, t_w1 - t_w0);  // vm wait + barrier
-    R32STAMP_ADD(stp, sslot + 3, 1ull);         // sub-chunks
-    R32STAMP_ADD(stp, 31, t_d0 - t_f0);         // flush + pre (all phases)
+    R32STAMP_ADD(sacc, sslot, t_d1 - t_d0);      // DMA issue
+    R32STAMP_ADD(sacc, sslot + 1, t_w0 - t_d1);  // k-steps (MFMA + epilogue VALU + LDS reads + split)
+    R32STAMP_ADD(sacc, sslot + 2, t_w1 - t_w0);  // vm wait + barrier
+    R32STAMP_ADD(sacc, sslot + 3, 1ull);         // sub-chunks
+    R32STAMP_ADD(sacc, 31, t_d0 - t_f0);         // flush + pre (all phases)
 #else
-    (void)t_d0; (void)t_d1; (void)t_w0; (void)stp; (void)sslot; (void)t_f0;
+    (void)t_d0; (void)t_d1; (void)t_w0; (void)sacc; (void)sslot; (void)t_f0;
 #endif
     if constexpr (u + 1 < U) {
       // tile J's epilogue operands, read now for its epilogue in tile J+1
@@ -1881,21 +1923,22 @@ __device__ __forceinline__ void gemm32(const uint16_t* __restrict__ src,
       if constexpr (NEP > 0 && (u + 1) % NH == 0) ep_wait();
     }
 #ifdef NERFHIP_STAMPS
-    R32STAMP_ADD(stp, 27, MEMTIME() - t_w1);    // first fragment of the next sub-chunk
+    R32STAMP_ADD(sacc, 20, MEMTIME() - t_w1);    // first fragment of the next sub-chunk
 #endif
   });
   if (next) r32_prefetch(next, ring, tid);   // (wave-uniform)
   const unsigned long long t_e0 = MEMTIME();
-  if constexpr (JT >= 2) flush(ic<JT - 2>);
+  auto flush_all = [&](auto Jc) { static_for<0, 4>([&](auto tc) { flush(Jc, tc); }); };
+  if constexpr (JT >= 2) flush_all(ic<JT - 2>);
   if constexpr (NEP > 0) {
     epre(ic<JT - 1>, ep);
     asm volatile("s_waitcnt lgkmcnt(0)");
     ep_wait();
   }
   static_for<0, 16>([&](auto ec) { elem(ic<JT - 1>, ec, ep); });
-  flush(ic<JT - 1>);
+  flush_all(ic<JT - 1>);
 #ifdef NERFHIP_STAMPS
-  R32STAMP_ADD(stp, 28, MEMTIME() - t_e0);   // phase tails
+  R32STAMP_ADD(sacc, 28, MEMTIME() - t_e0);   // phase tails
 #else
   (void)t_e0;
 #endif
@@ -1915,6 +1958,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
 #else
   unsigned long long* const stp = nullptr;
 #endif
+  unsigned long long sacc[32] = {};   // register stamp sums (stamps builds only)
   R32STAMP(stp, 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1943,13 +1987,11 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
   float* SGt = SG + (int64_t)blk * D * 16 + tq;
   // private cos map [n_pad/32][W/32][4][64 lanes][4]: one 1 KB run per (tile, t)
   const int64_t coff = (int64_t)(r0 >> 5) * JW * 4 * 256 + lane * 4;
-  auto tile_store = [&](float* base, auto Jc, const float (&v)[16]) {
-    constexpr int J = decltype(Jc)::value;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const f4 x = {v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
-      sst4(base + (32 * J + 8 * t) * 16, quad_transpose(x, j));
-    }
+  // register group t (features 32J + 8t + 4h + 0..3) of a tile
+  auto tile_store = [&](float* base, auto Jc, auto tc, const float (&v)[16]) {
+    constexpr int J = decltype(Jc)::value, t = decltype(tc)::value;
+    const f4 x = {v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]};
+    sst4(base + (32 * J + 8 * t) * 16, quad_transpose(x, j));
   };
   // (element e of a tile is feature 32J + 8(e>>2) + 4h + (e&3))
   float ho[JW][16];    // a layer's output tiles (raw accumulators until their epilogue)
@@ -2004,14 +2046,25 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
     });
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]), "+v"(wb[3]),
                  "+v"(wb[4]), "+v"(wb[5]), "+v"(wb[6]), "+v"(wb[7]));
+    float c0[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const float z = __fadd_rn(__fmul_rn(x, epv(wb, e)), epv(wb + 4, e));
       float s, co;
       sincos_fast(__fmul_rn(om, z), &s, &co);
       ho[T][e] = s;
+      c0[e] = co;
     }
-    if (train) tile_store(SHt, Tc, ho[T]);
+    if (train) {
+      static_for<0, 4>([&](auto tc) { tile_store(SHt, Tc, tc, ho[T]); });
+      // cos(ωz0) for the layer-0 backward (the 16-row kernel recomputes it
+      // there; at one wave per SIMD that phase's k-steps were VALU-bound)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f4 v = {c0[4 * t], c0[4 * t + 1], c0[4 * t + 2], c0[4 * t + 3]};
+        cst4(SC + coff + (T * 4 + t) * 256, v);
+      }
+    }
   });
   R32STAMP(stp, 1);
 
@@ -2021,7 +2074,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
     float* SHi = SHt + (int64_t)i * WN;
     float* SCi = SC + (int64_t)i * WN + coff;
     float cp[16];
-    gemm32<W, JW, TRAIN ? 8 : 0, 0, 4, TRAIN ? 16 : 0>(
+    gemm32<W, JW, TRAIN ? 8 : 0, 0, 4, TRAIN ? 16 : 0, 8>(
         xsm(false, i), xsm(false, i + 1), ring, hb, ho, tid, lane, no_pre,
         bias_epre((uint32_t)((1 + i) * W)),
         [&](auto Jc, auto ec, const auto& ep) {
@@ -2033,17 +2086,14 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
           cp[e] = co;
         },
         done,
-        [&](auto Jc) {
-          constexpr int J = decltype(Jc)::value;
+        [&](auto Jc, auto tc) {
+          constexpr int J = decltype(Jc)::value, t = decltype(tc)::value;
           if (train) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const f4 v = {cp[4 * t], cp[4 * t + 1], cp[4 * t + 2], cp[4 * t + 3]};
-              cst4(SCi + (J * 4 + t) * 256, v);
-            }
-            tile_store(SHi, Jc, ho[J]);
+            const f4 v = {cp[4 * t], cp[4 * t + 1], cp[4 * t + 2], cp[4 * t + 3]};
+            cst4(SCi + (J * 4 + t) * 256, v);
+            tile_store(SHi, Jc, tc, ho[J]);
           }
-        }, stp, 8);
+        }, sacc);
   }
 
   // ---- final nn.Linear(W, D): ŷᵀ = W_f·H_Lᵀ + b_f ; MSE ; dL/dŷ
@@ -2055,7 +2105,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
   float pv[2][16];     // per-lane operands of tiles J (J & 1), loaded a tile ahead
   float yp[16];
   float sq = 0.f;
-  gemm32<W, JD, TRAIN ? 4 : 0, TRAIN ? 4 : 0, 4, TRAIN ? 16 : 0>(
+  gemm32<W, JD, TRAIN ? 4 : 0, TRAIN ? 4 : 0, 4, TRAIN ? 16 : 0, 12>(
       xsm(false, L + 1), train ? xsm(true, L + 1) : nullptr, ring, hb, ho, tid, lane,
       [&](auto Jc) {
         constexpr int J = decltype(Jc)::value;
@@ -2080,17 +2130,14 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
         }
       },
       done,
-      [&](auto Jc) {
-        constexpr int J = decltype(Jc)::value;
+      [&](auto Jc, auto tc) {
+        constexpr int J = decltype(Jc)::value, t = decltype(tc)::value;
         if (has_y) {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const f4 v = {yp[4 * t], yp[4 * t + 1], yp[4 * t + 2], yp[4 * t + 3]};
-            st4(yo + 32 * J + 8 * t, v);      // ŷ[r][32J + 8t + 4h + q]
-          }
+          const f4 v = {yp[4 * t], yp[4 * t + 1], yp[4 * t + 2], yp[4 * t + 3]};
+          st4(yo + 32 * J + 8 * t, v);        // ŷ[r][32J + 8t + 4h + q]
         }
-        if (train) tile_store(SGt, Jc, ho[J]);
-      }, stp, 12);
+        if (train) tile_store(SGt, Jc, tc, ho[J]);
+      }, sacc);
   R32STAMP(stp, 3);
   if (!train) return;
   // loss partials per 16-row block: lanes 0..15 (and their h = 1 partners)
@@ -2108,7 +2155,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
     constexpr int K = decltype(Kc)::value;
     const float* SCl = SC + (int64_t)layer * WN + coff;
     float* SZl = SZt + (int64_t)layer * WN;
-    gemm32<K, JW, 4, 4, 0, 8>(
+    gemm32<K, JW, 4, 4, 0, 8, 16>(
         Mt, next, ring, hb, ho, tid, lane,
         [&](auto Jc) {
           constexpr int J = decltype(Jc)::value;
@@ -2124,14 +2171,14 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
           constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
           ho[J][e] = __fmul_rn(__fmul_rn(ho[J][e], pv[J & 1][e]), om);
         },
-        done, [&](auto Jc) { tile_store(SZl, Jc, ho[decltype(Jc)::value]); }, stp, 16);
+        done, [&](auto Jc, auto tc) { tile_store(SZl, Jc, tc, ho[decltype(Jc)::value]); }, sacc);
   };
   bwd(xsm(true, L + 1), xsm(true, L), ic<D>, L);               // W_fᵀ [W][D]
   R32STAMP(stp, 4);
   for (int i = L; i >= 2; --i) bwd(xsm(true, i), xsm(true, i - 1), ic<W>, i - 1);
 
-  // layer 0: cos(ω(x·w0 + b0)) recomputed with the forward's exact op
-  // sequence; dZ0 is only ever summed (dw0 = Σ dZ0·x, db0 = Σ dZ0), so each
+  // layer 0: cos(ωz0) from the forward's cos map; dZ0 is only ever summed
+  // (dw0 = Σ dZ0·x, db0 = Σ dZ0), so each
   // tile's 16 × 2 per-row values are reduce-scattered over the 16 lanes of a
   // 16-row block (xor 8, 4, 2, 1) and stored as [n_pad/16][2][W] partials:
   // lane c ends with the sums of registers 2(c & 7), 2(c & 7) + 1 — two
@@ -2139,26 +2186,27 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
   const int c16 = lane & 15;
   float* PZ = SZ + (int64_t)blk * 2 * W + (c16 >> 3) * W + 4 * h + 8 * ((c16 >> 1) & 3) +
               2 * (c16 & 1);
-  gemm32<W, JW, 1, 0, 8, 8>(
-      xsm(true, 1), nullptr, ring, hb, ho, tid, lane, no_pre,
-      [&](auto Jc, u4 (&ep)[8]) {              // w0 (ep[t]) and b0 (ep[4 + t]) of tile J
-        constexpr int J = decltype(Jc)::value;
-        static_for<0, 4>([&](auto tc) {
-          constexpr int t = decltype(tc)::value;
-          ep[t] = ds_read16<(32 * J + 8 * t) * 4>(bias_lane);
-          ep[4 + t] = ds_read16<(W + 32 * J + 8 * t) * 4>(bias_lane);
-        });
-      },
-      [&](auto Jc, auto ec, const auto& ep) {
-        constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
-        const float z = __fadd_rn(__fmul_rn(x, epv(ep, e)), epv(ep + 4, e));
-        float s, co;
-        sincos_fast(__fmul_rn(om, z), &s, &co);
-        ho[J][e] = __fmul_rn(__fmul_rn(ho[J][e], co), om);
-      },
-      done,
+  const float* SC0 = SC + coff;
+  gemm32<W, JW, 1, 4, 0, 8, 24>(
+      xsm(true, 1), nullptr, ring, hb, ho, tid, lane,
       [&](auto Jc) {
         constexpr int J = decltype(Jc)::value;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f4 v = ld4(SC0 + (J * 4 + t) * 256);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pv[J & 1][4 * t + q] = v[q];
+        }
+      },
+      no_epre,
+      [&](auto Jc, auto ec, const auto&) {
+        constexpr int J = decltype(Jc)::value, e = decltype(ec)::value;
+        ho[J][e] = __fmul_rn(__fmul_rn(ho[J][e], pv[J & 1][e]), om);
+      },
+      done,
+      [&](auto Jc, auto tc) {
+        constexpr int J = decltype(Jc)::value;
+        if constexpr (decltype(tc)::value != 0) return;   // the whole tile at t = 0
         float v[32];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -2182,8 +2230,13 @@ __global__ void __launch_bounds__(256, 1) k_step_rows32(KArgs a) {
         typedef float f2 __attribute__((ext_vector_type(2)));
         const f2 o2 = {w2[0], w2[1]};
         __builtin_nontemporal_store(o2, reinterpret_cast<f2*>(PZ + 32 * J));
-      }, stp, 24);
+      }, sacc);
   R32STAMP(stp, 5);
+#ifdef NERFHIP_STAMPS
+  if (stp && (threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 8; q < 32; ++q) stp[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32 + q] = sacc[q];
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3016,10 +3069,14 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   a.wsplit = static_cast<uint16_t*>(g->wsplit);
   a.rows_ks = rows_ks_for(g, s) ? 1 : 0;
   a.rows32 = rows32_for(g, s, a.rows_ks != 0) ? 1 : 0;
-  // NERFHIP_ROWS_LDS_PAD / NERFHIP_PARAMS_LDS_PAD: dynamic LDS per workgroup
-  // of the regular row / parameter kernels, KB (schedule experiments)
-  if (const char* e = getenv("NERFHIP_ROWS_LDS_PAD")) a.rows_dyn_lds = 1024u * (uint32_t)atoi(e);
-  if (const char* e = getenv("NERFHIP_PARAMS_LDS_PAD")) a.params_dyn_lds = 1024u * (uint32_t)atoi(e);
+#ifdef NERFHIP_DIAG_ENV
+  // diagnostic builds only — NERFHIP_ROWS_LDS_PAD / NERFHIP_PARAMS_LDS_PAD:
+  // dynamic LDS per workgroup of the regular row / parameter kernels, KB
+  // (schedule experiments), clamped to the CU's 160 KB
+  auto pad_kb = [](const char* e) { const int k = atoi(e); return 1024u * (uint32_t)(k < 0 ? 0 : k > 96 ? 96 : k); };
+  if (const char* e = getenv("NERFHIP_ROWS_LDS_PAD")) a.rows_dyn_lds = pad_kb(e);
+  if (const char* e = getenv("NERFHIP_PARAMS_LDS_PAD")) a.params_dyn_lds = pad_kb(e);
+#endif
 #ifdef NERFHIP_STAMPS
   if (const char* e = getenv("NERFHIP_PSTAMPS"))
     a.pstamps = reinterpret_cast<unsigned long long*>(strtoull(e, nullptr, 0));
@@ -3051,7 +3108,14 @@ int launch_rows(const KArgs& a, hipStream_t st) {
       // only) drops the padding so that two workgroups may share a CU.
       const char* e = getenv("NERFHIP_KS_SHARE_CU");
       unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;
-      if (const char* k = getenv("NERFHIP_KS_PAD_KB")) dyn = 1024u * (unsigned)atoi(k);   // diagnostics
+#ifdef NERFHIP_DIAG_ENV
+      // diagnostic builds only: an explicit pad (clamped to what fits the CU)
+      if (const char* k = getenv("NERFHIP_KS_PAD_KB")) {
+        const int kb = atoi(k);
+        dyn = 1024u * (unsigned)(kb < 0 ? 0 : kb) < kKsDynLds ? 1024u * (unsigned)(kb < 0 ? 0 : kb)
+                                                             : kKsDynLds;
+      }
+#endif
 #ifdef NERFHIP_EXP_KS_MODES
       if (a.mode == 0)
         hipLaunchKernelGGL((k_step_rows_ks<W, D, 0>), dim3(grid), dim3(256), dyn, st, a);
@@ -3250,7 +3314,7 @@ int nerfhip_build_flags(void) {
 #ifdef NERFHIP_STAMPS
   f |= NERFHIP_BUILD_STAMPS;
 #endif
-#if defined(NERFHIP_DIAG_ROWS_TWICE)
+#if defined(NERFHIP_DIAG_ROWS_TWICE) || defined(NERFHIP_DIAG_ENV)
   f |= NERFHIP_BUILD_DIAG;
 #endif
   return f;

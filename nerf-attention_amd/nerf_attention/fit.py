@@ -323,8 +323,9 @@ def _print_summary(all_results: list[dict], layers_to_fit: list[int]) -> None:
 
 def main() -> None:
     # one HIP hardware queue per group stream (before the runtime initialises;
-    # raised from HIP's default of 4, see bench.py)
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    # unset or HIP's default of 4 is raised to 8, any other value wins; see bench.py)
+    if (os.environ.get("NERFHIP_KEEP_HW_QUEUES") != "1"
+            and os.environ.get("GPU_MAX_HW_QUEUES", "").strip() in ("", "4")):
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
     parser = argparse.ArgumentParser(description='Fit SIRENs to KV cache')
     parser.add_argument('--kv_dir', type=str, default='results/kv_cache')

@@ -152,14 +152,11 @@ _LEFT, _SEEDED, _NEXT = slice(8, 12), slice(12, 16), slice(16, 24)   # u64 next,
 _STATE_BYTES = 5056                                                    # normal-sample cache
 
 
-def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
-    """The flat initial parameters `SIREN(config, out_features)` would hold
-    (state_dict order), drawn from — and advancing — torch's default CPU
-    generator exactly as that constructor does, without building the module:
-    nerfhip_rng_uniform_segments replays torch's mt19937 + uniform_ on the
-    host at the bare generator's speed (bit-identical, tests/test_host.py).
-    The sweep's drivers use it to overlap the inits with training."""
-    segs = _init_segments(config, out_features)
+def _replay(segs) -> torch.Tensor | None:
+    """Draw the segments (count, bound, kept) through the native replay of
+    torch's default CPU generator, advancing it; None (and nothing drawn)
+    when the generator state is not the CPUGeneratorImplState layout this
+    replay reads (another torch build)."""
     counts = np.array([c for c, _b, _k in segs], dtype=np.int64)
     bounds = np.array([b for _c, b, _k in segs], dtype=np.float64)
     offs, off = np.full(len(segs), -1, dtype=np.int64), 0
@@ -168,9 +165,7 @@ def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
             offs[i], off = off, off + c
     raw = torch.get_rng_state().numpy().copy()
     if raw.size != _STATE_BYTES or raw[_SEEDED].view(np.int32)[0] != 1:
-        # not the CPUGeneratorImplState layout this replay reads (another torch
-        # build): draw through the module itself, which is exact by definition
-        return SIREN(config, out_features).flat_parameters()
+        return None
     flat = torch.empty(off, dtype=torch.float32)
     state = raw[_STATE].view(np.uint64).astype(np.uint32)
     left = ctypes.c_int32(int(raw[_LEFT].view(np.int32)[0]))
@@ -185,6 +180,50 @@ def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
     raw[_NEXT].view(np.uint64)[0] = nxt.value
     torch.set_rng_state(torch.from_numpy(raw))
     return flat
+
+
+_REPLAY_OK = None
+
+
+def replay_matches_torch() -> bool:
+    """One-time self-check of the native replay against torch's own uniform_
+    on this host: the replay reproduces the rounding of torch's CPU kernel
+    (x·span + lo contracted into one fma, as its AVX2 / AVX-512 paths do);
+    under another kernel (ATEN_CPU_CAPABILITY=default, a host without FMA, a
+    different torch) the bits could differ, and init_flat then builds the
+    modules instead.  Shapes of SIREN layers: a discarded reset segment, a
+    W x W weight, a bias, a short tail.  The caller's generator state is
+    restored."""
+    global _REPLAY_OK
+    if _REPLAY_OK is None:
+        probe = [(300, 0.0, False), (256 * 256, 0.05, True), (256, 0.05, True), (17, 1.0, True)]
+        saved = torch.get_rng_state()
+        try:
+            torch.manual_seed(20240601)
+            ref = [torch.empty(n).uniform_(-b, b) for n, b, _k in probe]
+            torch.manual_seed(20240601)
+            got = _replay(probe)
+            _REPLAY_OK = got is not None and torch.equal(got, torch.cat(ref[1:]))
+        finally:
+            torch.set_rng_state(saved)
+    return _REPLAY_OK
+
+
+def init_flat(config: SIRENConfig, out_features: int) -> torch.Tensor:
+    """The flat initial parameters `SIREN(config, out_features)` would hold
+    (state_dict order), drawn from — and advancing — torch's default CPU
+    generator exactly as that constructor does, without building the module:
+    nerfhip_rng_uniform_segments replays torch's mt19937 + uniform_ on the
+    host at the bare generator's speed (bit-identical, tests/test_host.py).
+    The sweep's drivers use it to overlap the inits with training.  Where the
+    replay cannot be shown to match torch's own kernel on this host
+    (replay_matches_torch), or the generator state layout differs, it builds
+    the module instead, which is exact by definition."""
+    if replay_matches_torch():
+        flat = _replay(_init_segments(config, out_features))
+        if flat is not None:
+            return flat
+    return SIREN(config, out_features).flat_parameters()
 
 
 def uninitialised(config: SIRENConfig, out_features: int, device) -> SIREN:

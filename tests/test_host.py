@@ -442,3 +442,24 @@ def test_synthetic_spawn_pool_bitwise_and_leaves_nothing(monkeypatch):
     assert set(glob.glob("/dev/shm/nerf_synth_*")) == before
     from multiprocessing import resource_tracker
     assert getattr(resource_tracker._resource_tracker, "_pid", None) is None
+
+
+def test_init_replay_self_check(monkeypatch):
+    """init_flat's one-time self-check: the replay matches torch's uniform_
+    here (so init_flat takes it), leaves the caller's generator untouched,
+    and a failing check (a host whose torch kernel rounds differently) sends
+    init_flat to the module constructor — same bits either way."""
+    from nerf_attention import siren
+    monkeypatch.setattr(siren, "_REPLAY_OK", None)
+    torch.manual_seed(7)
+    before = torch.get_rng_state()
+    assert siren.replay_matches_torch()
+    assert torch.equal(before, torch.get_rng_state())
+    cfg = SIRENConfig(128, 2, 30.0, "t")
+    torch.manual_seed(3)
+    a = siren.init_flat(cfg, 64)
+    monkeypatch.setattr(siren, "_REPLAY_OK", False)
+    monkeypatch.setattr(siren, "_replay", lambda segs: (_ for _ in ()).throw(AssertionError))
+    torch.manual_seed(3)
+    b = siren.init_flat(cfg, 64)
+    assert torch.equal(a, b)

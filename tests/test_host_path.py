@@ -209,19 +209,25 @@ def test_bench_cpu_baseline_times_host_path():
     assert out["value"] > 0 and out["archs"] == 7
 
 
-@pytest.mark.parametrize("given,want", [(None, "8"), ("4", "8"), ("16", "16")])
-def test_bench_raises_hw_queues(given, want):
+@pytest.mark.parametrize("given,keep,want", [(None, None, "8"), ("4", None, "8"),
+                                             ("16", None, "16"), ("2", None, "2"),
+                                             ("4", "1", "4")])
+def test_bench_raises_hw_queues(given, keep, want):
     """bench.py gives every group stream its own hardware queue: it raises
-    GPU_MAX_HW_QUEUES to 8 when unset or lower (the GPU boxes export HIP's
-    default of 4) and keeps a higher setting."""
+    GPU_MAX_HW_QUEUES to 8 when unset or at HIP's default of 4 (what the GPU
+    boxes export); any other explicit value wins, and NERFHIP_KEEP_HW_QUEUES=1
+    keeps the default too."""
     import os
     import subprocess
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parent.parent
     env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    env.pop("NERFHIP_KEEP_HW_QUEUES", None)
     if given is not None:
         env["GPU_MAX_HW_QUEUES"] = given
+    if keep is not None:
+        env["NERFHIP_KEEP_HW_QUEUES"] = keep
     code = (f"import os, sys; sys.path.insert(0, {str(root)!r}); import bench; "
             "print(os.environ['GPU_MAX_HW_QUEUES'])")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,

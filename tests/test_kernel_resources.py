@@ -28,7 +28,9 @@ pytestmark = pytest.mark.skipif(
 KNOWN_SCRATCH = {
     "void k_step_rows<256, 128, true, true>(nerfhip_detail::KArgs)": 120,
     "void k_step_rows<256, 64, true, true>(nerfhip_detail::KArgs)": 120,
-    "void k_step_params<128, 128, true, false, false>(nerfhip_detail::KArgs)": 12,
+    "void k_step_params<128, 128, true, false, 0>(nerfhip_detail::KArgs)": 12,
+    # the opt-in 32-row kernel: one 8-byte spill slot at 512 registers
+    "void k_step_rows32<256, 128, true>(nerfhip_detail::KArgs)": 8,
 }
 
 
@@ -42,9 +44,13 @@ def test_every_step_kernel_present(ks):
     for k in ("k_step_rows<", "k_step_rows_ks<", "k_step_params<", "k_adam_split<",
               "k_transpose_params", "k_normalize", "k_row_metrics"):
         assert k in names, k
-    # the fused parameter step in the K-split layout (KSX) exists for every K-split width
+    # the fused parameter step in the K-split weight layout (KSX = kLayKs = 1)
+    # exists for every K-split width, and in the 32-row layout (kLay32 = 2) at W = 256
     for w in (128, 256, 512):
-        assert f"void k_step_params<{w}, 128, true, false, true>(nerfhip_detail::KArgs)" in ks
+        assert f"void k_step_params<{w}, 128, true, false, 1>(nerfhip_detail::KArgs)" in ks
+    assert "void k_step_params<256, 128, true, false, 2>(nerfhip_detail::KArgs)" in ks
+    for t in ("true", "false"):
+        assert f"void k_step_rows32<256, 128, {t}>(nerfhip_detail::KArgs)" in ks
 
 
 def test_no_unexpected_scratch(ks):

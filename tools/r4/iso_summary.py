@@ -18,6 +18,16 @@ from collections import defaultdict
 from pathlib import Path
 
 N_SIMD, N_XCD = 1024, 8
+ROOT = Path(__file__).resolve().parents[2]
+
+
+def lib_sha16() -> str:
+    """The measured library's hash (bench.py reports these counters only for
+    the same build)."""
+    import hashlib
+    import os
+    lib = os.environ.get("NERFHIP_LIB") or ROOT / "nerf-attention_amd/nerf_attention/_lib/libnerfhip.so"
+    return hashlib.sha256(Path(lib).read_bytes()).hexdigest()[:16]
 
 
 def main():
@@ -30,9 +40,14 @@ def main():
     kind = ev["kernel"].split("<")[0]
     x3 = "true" if ev["precision"] == "bf16x3" else "false"
     pat = re.compile(rf"{kind}<{W}, 128, {x3}, (true|false)(, false)*>" if kind == "k_step_rows"
-                     else rf"{kind}<{W}, 128, {x3}, false, false>")
+                     else rf"{kind}<{W}, 128, {x3}, false, false(, \d+)?>")
+    # the 32-row training kernel (k_step_rows32<W, 128, TRAIN>) stands in for
+    # k_step_rows when the library selects it
+    pat32 = re.compile(rf"k_step_rows32<{W}, 128, true>")
 
     def match(name):
+        if kind == "k_step_rows" and pat32.search(name):
+            return True
         m = pat.search(name)
         return bool(m) and (kind != "k_step_rows" or m.group(1) == "true")
 
@@ -64,6 +79,7 @@ def main():
         "hipevent_avg_ms": ev["avg_launch_ms"],
         "rocprof_vs_hipevent": stats and round(stats["avg_ms"] / ev["avg_launch_ms"] - 1, 4),
         "flops_per_launch": ev["flops_per_launch"], "fits": ev["fits"], "epochs": ev["epochs"],
+        "lib_sha16": lib_sha16(),
         "source": "tools/r4/iso_prof.sh (rocprofv3 of tools/r4/isokernel.py)"}}
     print(json.dumps(out, indent=1))
 

@@ -60,7 +60,7 @@ out["phase_tails_per_wave"] = round(float(st[:, 28].mean()))
 out["phase_head_wait_per_wave"] = round(float(st[:, 29].mean()))
 out["phase_head_split_per_wave"] = round(float(st[:, 30].mean()))
 out["flush_pre_per_wave"] = round(float(st[:, 31].mean()))
-out["next_fragment_per_wave"] = round(float(st[:, 27].mean()))
+out["next_fragment_per_wave"] = round(float(st[:, 20].mean()))
 out["waves"] = int(st.shape[0])
 out["spread_total"] = [round(float(np.percentile(st[:, 5] - st[:, 0], q))) for q in (5, 50, 95)]
 print(json.dumps(out, indent=1))
