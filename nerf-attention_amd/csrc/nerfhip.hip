@@ -84,6 +84,11 @@ struct KArgs {
   int32_t n_split;
   int64_t gp_stride;
   float* gpart;
+  // 1 = the last-arriving slice of each parameter tile sums the slabs and
+  // runs Adam itself (no k_adam_split launch); arrival counters, one int32
+  // per tile, live at gpart + fit·gp_stride + ctr_off
+  int32_t split_fused;
+  int64_t ctr_off;
   // bf16x3 precision (NERFHIP_PRECISION_BF16X3): every MFMA weight operand as
   // exact 3-way bf16 split planes, forward and transposed (xoff layout)
   int32_t x3;
@@ -530,15 +535,31 @@ __host__ __device__ inline int64_t n_params(int W, int D, int L) {
   return off_final_w(W, L) + (int64_t)W * D + D;
 }
 
+// A split-K partial-slab element.  For the fused reduction (split_finish)
+// the store is write-through (sc1: agent-scope relaxed), so the slices need no
+// L2 write-back (release fence) before their arrival — the fence costs each
+// arriving workgroup a write-back of its XCD's whole dirty L2
+// (cdna_hip_programming.md, in-launch split-K); k_adam_split's slabs cross a
+// kernel boundary and stay plain.
+__device__ __forceinline__ void slab_store(const nerfhip_detail::KArgs& a, float* p, float v) {
+  if (a.split_fused) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 // torch.optim.Adam, single-tensor path (the reference runs on CPU, where the
 // foreach/fused paths are unavailable): TORCH/optim/adam.py:457,476,531-547.
 __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g,
                                             float step_size, float bc2_sqrt) {
-  m = m + 0.1f * (g - m);                        // exp_avg.lerp_(grad, 1-β1)
-  v = v * 0.999f;                                // exp_avg_sq.mul_(β2)
-  v = v + (0.001f * g) * g;                      //   .addcmul_(grad, grad, 1-β2)
+  // The roundings are spelled out (explicit fma, no contraction): the same
+  // update is inlined into several kernels (the parameter tiles' epilogues,
+  // k_adam_split, the fused split-K reducer), and left to the contraction
+  // pass each copy could fuse differently — 1-ulp differences between paths
+  // that must agree bitwise (test_split_fused_equals_separate_pass).
+#pragma clang fp contract(off)
+  m = fmaf(0.1f, g - m, m);                      // exp_avg.lerp_(grad, 1-β1)
+  v = fmaf(0.001f * g, g, v * 0.999f);           // exp_avg_sq.mul_(β2).addcmul_(grad, grad, 1-β2)
   const float denom = sqrtf(v) / bc2_sqrt + 1e-8f;  // (√v / √bc2).add_(eps)
-  p = p + (-step_size) * (m / denom);            // addcdiv_(m, denom, -lr/bc1)
+  p = fmaf(-step_size, m / denom, p);            // addcdiv_(m, denom, -lr/bc1)
 }
 
 // ---------------------------------------------------------------------------
@@ -1233,10 +1254,19 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
 // Dynamic LDS of every K-split workgroup: with its static LDS (≤ 24 592 B
 // at W = 512: partials, finalised tiles, bias) it takes the CU's whole
 // 160 KB, so a K-split workgroup never shares a CU with any workgroup that
-// uses LDS — its own kind or another kernel's (a compile-time
-// forward-only instantiation of this kernel gave wrong blocks when two
-// workgroups shared a CU, and the cause is below the ISA's ordering model).
-constexpr unsigned kKsDynLds = 163840u - 24592u;
+// uses LDS — its own kind or another kernel's.  Containment kept from the
+// co-residency fault: a compile-time forward-only
+// instantiation gave wrong blocks when two workgroups shared a CU; the cause
+// was the SGPR-soffset rewrite right after a buffer load (KsPhase), which the
+// source no longer produces, and the LDS protocol carries no cross-wave race
+// (tools/r5/ks_lds_hb.py).  launch_rows also caps the pad at what the
+// kernel's actual static LDS leaves.
+#ifdef NERFHIP_EXP_KS_TRACE
+constexpr unsigned kKsTraceLds = 64u;   // the trace build's ks_tr_* state (below)
+#else
+constexpr unsigned kKsTraceLds = 0u;
+#endif
+constexpr unsigned kKsDynLds = 163840u - 24592u - kKsTraceLds;
 template <int W> struct KsCfg {
   // A-fragment items (S8) in flight per wave.  (W = 256: 10 and 12 items
   // measured 3.5 % and 7 % slower than 6 on one medium fit: not load-latency
@@ -1252,13 +1282,43 @@ template <int W> struct KsCfg {
 __host__ __device__ constexpr int ks_owner(int J) { return (J >> 1) & 3; }
 __host__ __device__ constexpr int ks_local(int J) { return 2 * (J >> 3) + (J & 1); }
 
+#ifdef NERFHIP_EXP_KS_TRACE
+// Diagnostic build: every LDS access of the K-split kernel traced per lane —
+// (barrier count, read/write, LDS byte address) — for two workgroups of each
+// mode's launch; tools/r5/ks_lds_hb.py checks that every cross-wave
+// write→read and read→overwrite pair of an address is separated by a barrier.
+constexpr int kKsTrMax = 4096;   // events per wave
+__shared__ uint32_t* ks_tr_buf;
+__shared__ int ks_tr_n[4], ks_tr_bc[4];
+__device__ __forceinline__ void ks_tr(const void* p, int rw) {
+  uint32_t* b = ks_tr_buf;
+  if (!b) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = ks_tr_n[w];
+  if (n < kKsTrMax)
+    b[((int64_t)w * kKsTrMax + n) * 64 + lane] =
+        ((uint32_t)ks_tr_bc[w] << 18) | ((uint32_t)rw << 17) | ((uint32_t)(uintptr_t)p & 0x1ffffu);
+  ks_tr_n[w] = n + 1;
+}
+__device__ __forceinline__ void ks_tr_barrier() { ks_tr_bc[threadIdx.x >> 6] += 1; }
+#define KS_TR(p, rw) ks_tr((p), (rw))
+#else
+#define KS_TR(p, rw) ((void)0)
+__device__ __forceinline__ void ks_tr_barrier() {}
+#endif
+
 __device__ __forceinline__ void ks_barrier() {
 #ifdef NERFHIP_EXP_KS_VMWAIT   // diagnostic: also drain vector memory
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  ks_tr_barrier();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void ks_sync() {
+  ks_tr_barrier();
+  __syncthreads();
 }
 
 // A phase's bias vector (N floats, N compile-time) global → LDS with no
@@ -1275,6 +1335,8 @@ __device__ __forceinline__ void ks_stage(float* dst, const float* src, int w, in
   constexpr int WAVES = N >= 256 ? 4 : N / 64, E = N / (64 * WAVES);
   if (w < WAVES) {                                 // w: an SGPR (readfirstlane)
     const int i = (w * 64 + lane) * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) KS_TR(dst + i + e, 1);
     if constexpr (E == 4) st4(dst + i, ld4(src + i));
     else if constexpr (E == 2) {
       const float2 v = *reinterpret_cast<const float2*>(src + i);
@@ -1364,12 +1426,15 @@ __device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ xs, int src
   auto slot = [](int J) { return 2 * ((J >> 1) & 1) + (J & 1); };
   auto finalize = [&](int J, float pv) {
     const float* p = part + slot(J) * 1024 + w * 64 + lane;
+    KS_TR(p, 0); KS_TR(p + 256, 0); KS_TR(p + 512, 0); KS_TR(p + 768, 0);
     const float acc = ((p[0] + p[256]) + p[512]) + p[768];
+    KS_TR(outb + slot(J) * 256 + w * 64 + lane, 1);
     outb[slot(J) * 256 + w * 64 + lane] = fin(J, acc, pv);
   };
   auto owner_read = [&](int J) {
     if (w == ks_owner(J)) {
       const float* o = outb + slot(J) * 256 + lane;
+      KS_TR(o, 0); KS_TR(o + 64, 0); KS_TR(o + 128, 0); KS_TR(o + 192, 0);
       const f4 v = {o[0], o[64], o[128], o[192]};
       own(J, v);
     }
@@ -1395,7 +1460,10 @@ __device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ xs, int src
     for (int t = 0; t < 2; ++t) {
       float* pw = part + slot(2 * Pp + t) * 1024 + w * 256 + lane;   // part[slot][w][q][lane]
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pw[q * 64] = acc[t][q];
+      for (int q = 0; q < 4; ++q) {
+        KS_TR(pw + q * 64, 1);
+        pw[q * 64] = acc[t][q];
+      }
       pv_prev[t] = pv[t];
     }
     ks_barrier();
@@ -1487,10 +1555,19 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   // matrix offsets of the fit's split weights (bf16 elements; < 2^31 bytes)
   auto xm = [&](bool bwd_mat, int i) { return (int)xs_mat(W, D, L, bwd_mat, i); };
   ks_prefetch<W>(ring, XS, xm(false, 1), c, g, w);
+#ifdef NERFHIP_EXP_KS_TRACE
+  if (tid == 0)
+    ks_tr_buf = a.pstamps && blockIdx.x < 2
+                    ? reinterpret_cast<uint32_t*>(a.pstamps) +
+                          (int64_t)(2 * a.mode + blockIdx.x) * 4 * kKsTrMax * 64
+                    : nullptr;
+  if (tid < 4) ks_tr_n[tid] = ks_tr_bc[tid] = 0;
+  __syncthreads();
+#endif
 
   // ---- layer 0 (K = 1, VALU): this wave's tiles J = 2s + h, s = w + 4m
   ks_stage<2 * W>(bias, P, w, lane);
-  __syncthreads();
+  ks_sync();
   const float x = a.pos[r];
   float* SHt = SH + (int64_t)rblk * W * 16 + g * 64 + (c & 3) * 16 + (c >> 2) * 4;
 #pragma unroll
@@ -1499,6 +1576,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int f = 16 * J + 4 * g + q;
+      KS_TR(bias + f, 0); KS_TR(bias + W + f, 0);
       const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
       float s, co;
       sincos_fast(__fmul_rn(om, z), &s, &co);
@@ -1510,7 +1588,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
     }
   }
   split_out(ic<W / 128>);
-  __syncthreads();
+  ks_sync();
   KSTAMP(1);
 
   // ---- hidden SineLayers 1..L
@@ -1522,6 +1600,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
         XS, xm(false, i), hs, ring, xm(false, i + 1), w, c, g,
         lane, part, outb, no_pre,
         [&](int J, float acc, float) {
+          KS_TR(bias + 16 * J + fe, 0);
           const float z = __fadd_rn(acc, bias[16 * J + fe]);
           float s, co;
           sincos_fast(__fmul_rn(om, z), &s, &co);
@@ -1551,6 +1630,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
       lane, part, outb,
       [&](int J) { return train_f ? T[16 * J] : 0.f; },
       [&](int J, float acc, float t) {
+        KS_TR(bias + 16 * J + fe, 0);
         const float y = __fadd_rn(acc, bias[16 * J + fe]);
         if (has_y) yo[16 * J] = y;
         float gv = 0.f;
@@ -1566,6 +1646,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   KSTAMP(3);
   if (!train_f) return;
   sq = wave_sum(sq);
+  KS_TR(lsum + w, 1);
   lsum[w] = sq;                  // every lane holds the wave's sum
   ys[0] = split_pair(ho[0], ho[1]);
 
@@ -1597,6 +1678,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
       XS, xm(true, 1), hs, ring, -1, w, c, g, lane, part, outb, no_pre,
       [&](int J, float acc, float) {
         const int f = 16 * J + fe;
+        KS_TR(bias + f, 0); KS_TR(bias + W + f, 0);
         const float z = __fadd_rn(__fmul_rn(x, bias[f]), bias[W + f]);
         float s, co;
         sincos_fast(__fmul_rn(om, z), &s, &co);
@@ -1614,9 +1696,11 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
         return 0.f;
       },
       [](int, f4) {});
-  if (w == 0)                    // scalar branch; the wave's lanes store one value
+  if (w == 0) {                  // scalar branch; the wave's lanes store one value
+    KS_TR(lsum, 0); KS_TR(lsum + 1, 0); KS_TR(lsum + 2, 0); KS_TR(lsum + 3, 0);
     a.loss_partial[fit * a.lp_stride + (int64_t)a.epoch * (n_pad / 16) + rblk] =
         ((lsum[0] + lsum[1]) + lsum[2]) + lsum[3];
+  }
   KSTAMP(6);
 }
 
@@ -2399,7 +2483,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
           const int j = jrow0 + qq + 8 * qb + 4 * h;
           const int64_t idx = pw + (int64_t)j * a.W + kcol;
           if (G) {
-            G[idx] = acc[x][y][qb * 4 + qq];
+            slab_store(a, G + idx, acc[x][y][qb * 4 + qq]);
             continue;
           }
           float p = P[idx], mm = M[idx], vv = V[idx];
@@ -2417,7 +2501,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
       if (h == 0) {
         const int64_t idx = pb + j0 + wj * (TJ / 2) + 32 * x + lr;
         if (G) {
-          G[idx] = s;
+          slab_store(a, G + idx, s);
           continue;
         }
         float p = P[idx], mm = M[idx], vv = V[idx];
@@ -2597,7 +2681,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           const int64_t idx = pw + (int64_t)j * W + kcol;
           const float gsum = hi[x][y][qb * 4 + qq] + lo[x][y][qb * 4 + qq];
           if (G) {
-            G[idx] = gsum;
+            slab_store(a, G + idx, gsum);
             continue;
           }
           float p = P[idx], mm = M[idx], vv = V[idx];
@@ -2631,7 +2715,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
       if ((tid & 3) == 0 && tid + NTH * m < NA4) {
         const int64_t idx = pb + j0 + (stage_slot<true>(tid + NTH * m) >> 2);
         if (G) {
-          G[idx] = s;
+          slab_store(a, G + idx, s);
         } else {
           float p = P[idx], mm = M[idx], vv = V[idx];
           adam_update(p, mm, vv, s, step_size, bc2s);
@@ -2641,6 +2725,170 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     }
   }
   PSTAMP(4);
+}
+
+// Fused split-K reduction (KArgs.split_fused): the slices of one parameter
+// tile arrive in any order; each publishes its partial slab (release fence,
+// then one agent-scope atomic add on the tile's counter) and the last to
+// arrive (acquire) sums the n_split slabs of the tile in slice order —
+// exactly k_adam_split's order, so the result is bitwise the same — runs Adam
+// and writes the weight copies.
+// NS slices compile-time: every slice's load of a 4-parameter batch in flight.
+template <int NS, int W, int D, bool X3>
+__device__ __forceinline__ void split_finish_run(const KArgs& a, int fit, int L, int64_t pw,
+                                                 int rows, int cols, int j0, int k0, int layer,
+                                                 int nbias, int64_t pb) {
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const float* g = a.gpart + fit * a.gp_stride;
+  float* P = a.params + fit * a.p_stride;
+  float* M = a.m + fit * a.p_stride;
+  float* V = a.v + fit * a.p_stride;
+  float* PT = a.params_t + fit * a.pt_stride;
+  uint16_t* XS = X3 ? a.wsplit + fit * a.ws_stride : nullptr;
+  const float step_size = a.sched[2 * a.epoch], bc2s = a.sched[2 * a.epoch + 1];
+  const int lay = wlayout(a);
+  const int64_t ps = a.p_stride;
+  // biases first, their loads in flight beside the first weight batch (a
+  // clamped index, not a branch around the loads)
+  const bool hb = tid < nbias;
+  const int64_t ib = pb + (hb ? tid : 0);
+  float bg[NS];
+#pragma unroll
+  for (int sp = 0; sp < NS; ++sp) bg[sp] = g[sp * ps + ib];
+  float bp = P[ib], bm = M[ib], bv = V[ib];
+  // weights as 16-B runs along k (cols is a multiple of 64, every run aligned):
+  // a thread's whole batch — B runs × NS slabs, and P/M/V — is loaded before
+  // any is used, so a batch costs one dependent round trip
+  const int n4 = rows * cols / 4;
+  constexpr int B = 16 / NS > 0 ? 16 / NS : 1;   // <= 16 slab runs (64 floats) in flight
+  for (int q0 = tid; q0 < n4; q0 += B * nth) {
+    f4 gv[B][NS], pv[B], mv[B], vv[B];
+    int64_t ix[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const int q = q0 + b * nth < n4 ? q0 + b * nth : q0;
+      const int e = 4 * q;
+      ix[b] = pw + (int64_t)(j0 + e / cols) * W + k0 + e % cols;
+#pragma unroll
+      for (int sp = 0; sp < NS; ++sp) gv[b][sp] = *reinterpret_cast<const f4*>(g + sp * ps + ix[b]);
+      pv[b] = *reinterpret_cast<const f4*>(P + ix[b]);
+      mv[b] = *reinterpret_cast<const f4*>(M + ix[b]);
+      vv[b] = *reinterpret_cast<const f4*>(V + ix[b]);
+    }
+    if (q0 == tid && hb) {
+      float gs = bg[0];
+#pragma unroll
+      for (int sp = 1; sp < NS; ++sp) gs += bg[sp];   // slice order
+      adam_update(bp, bm, bv, gs, step_size, bc2s);
+      P[ib] = bp; M[ib] = bm; V[ib] = bv;
+    }
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      if (q0 + b * nth >= n4) break;
+      const int e = 4 * (q0 + b * nth);
+      const int j = j0 + e / cols, k = k0 + e % cols;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float gs = gv[b][0][c];
+#pragma unroll
+        for (int sp = 1; sp < NS; ++sp) gs += gv[b][sp][c];   // slice order
+        float p = pv[b][c], mm = mv[b][c], v2 = vv[b][c];
+        adam_update(p, mm, v2, gs, step_size, bc2s);
+        pv[b][c] = p; mv[b][c] = mm; vv[b][c] = v2;
+      }
+      *reinterpret_cast<f4*>(P + ix[b]) = pv[b];
+      *reinterpret_cast<f4*>(M + ix[b]) = mv[b];
+      *reinterpret_cast<f4*>(V + ix[b]) = vv[b];
+      if (layer > 0) {
+        const float p4[4] = {pv[b][0], pv[b][1], pv[b][2], pv[b][3]};
+        if constexpr (X3) {
+          // the layout as a compile-time constant per branch (a run-time
+          // select inside the unrolled copies spills them to scratch)
+          auto copies = [&](auto lay_c) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) put_w(XS, decltype(lay_c)::value, W, D, L, layer, j, k + c, p4[c]);
+          };
+          if (lay == kLayKs) copies(std::integral_constant<int, kLayKs>{});
+          else if (lay == kLay32) copies(std::integral_constant<int, kLay32>{});
+          else copies(std::integral_constant<int, kLayX>{});
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (layer <= L) PT[(int64_t)(layer - 1) * W * W + (int64_t)(k + c) * W + j] = p4[c];
+            else PT[(int64_t)L * W * W + (int64_t)(k + c) * D + j] = p4[c];
+          }
+        }
+      }
+    }
+  }
+  if (tid >= n4 && hb) {   // (only if some bias thread had no weight batch)
+    float gs = bg[0];
+#pragma unroll
+    for (int sp = 1; sp < NS; ++sp) gs += bg[sp];
+    adam_update(bp, bm, bv, gs, step_size, bc2s);
+    P[ib] = bp; M[ib] = bm; V[ib] = bv;
+  }
+}
+
+// Arrival + (if last) the tile's reduction.  Tile t of ParamsCfg C: hidden
+// layer tiles, then the final layer's, then the first layer's (k_step_params).
+// The hand-off is cdna_hip_programming.md's in-launch split-K recipe in its
+// write-through form: the slabs were stored sc1 (slab_store), every wave
+// drains them (vmcnt 0), then one lane draws a ticket from the tile's
+// monotonic counter (agent-scope relaxed add, no release fence needed), and
+// the reducer's lane acquires (this CU's L1 invalidated) before any wave
+// reads a slab.  The "I am last" word lives in the block's one LDS array (a second
+// __shared__ object can de-pipeline the staging loop).
+template <class C, int W, int D, bool X3>
+__device__ void split_finish(const KArgs& a, int fit, int L, int t, float* lds) {
+  int* flag = reinterpret_cast<int*>(lds);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave's stores drained; the staging array is free
+  if (threadIdx.x == 0) {
+    // the counter only grows (zeroed by the prologue): epoch e's last
+    // arrival is the one that brings it to (e + 1) · n_split
+    int* ctr = reinterpret_cast<int*>(a.gpart + fit * a.gp_stride + a.ctr_off) + t;
+    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (old + 1) % a.n_split == 0;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  // weights: rows × cols at pw + (j0 + r)·W + k0 + c; biases: nbias at pb
+  int64_t pw, pb;
+  int rows, cols, j0, k0, layer, nbias;
+  if (t < L * C::TH) {
+    const int u = t % C::TH;
+    layer = t / C::TH + 1;
+    pw = off_hidden_w(W, layer);
+    rows = C::T; cols = C::TK; j0 = (u / C::NTK) * C::T; k0 = (u % C::NTK) * C::TK;
+    pb = pw + (int64_t)W * W + j0;
+    nbias = (u % C::NTK) == 0 ? rows : 0;
+  } else if (t < L * C::TH + C::TF) {
+    const int u = t - L * C::TH;
+    layer = L + 1;
+    pw = off_final_w(W, L);
+    rows = C::TD; cols = C::TK; j0 = (u / C::NTK) * C::TD; k0 = (u % C::NTK) * C::TK;
+    pb = pw + (int64_t)W * D + j0;
+    nbias = (u % C::NTK) == 0 ? rows : 0;
+  } else {
+    // first layer, features f0 .. f0 + 16·NW: w0[f] at f, b0[f] at W + f
+    const int f0 = (t - L * C::TH - C::TF) * (16 * C::NW);
+    layer = 0;
+    pw = 0; rows = 1; cols = 16 * C::NW; j0 = 0; k0 = f0;
+    pb = W + f0;
+    nbias = 16 * C::NW;
+  }
+  switch (a.n_split) {
+    case 2: split_finish_run<2, W, D, X3>(a, fit, L, pw, rows, cols, j0, k0, layer, nbias, pb); break;
+    case 4: split_finish_run<4, W, D, X3>(a, fit, L, pw, rows, cols, j0, k0, layer, nbias, pb); break;
+    case 8: split_finish_run<8, W, D, X3>(a, fit, L, pw, rows, cols, j0, k0, layer, nbias, pb); break;
+    default: split_finish_run<16, W, D, X3>(a, fit, L, pw, rows, cols, j0, k0, layer, nbias, pb); break;
+  }
 }
 
 // Tiles: dW[j0:j0+T][k0:k0+TK] on 4 waves, two workgroups per CU.  (WIDE:
@@ -2663,7 +2911,9 @@ template <int W, int D, bool X3, bool SMALL = false> struct ParamsCfg {
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
-template <int W, int D, bool X3, bool SMALL = false, int KSX = kLayX>
+// SK: the split-K instantiation (launched only for n_split > 1: partial slabs,
+// and the fused reduction); the unsplit one has no slab path at all.
+template <int W, int D, bool X3, bool SMALL = false, int KSX = kLayX, bool SK = SMALL>
 __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
                                   (ParamsCfg<W, D, X3, SMALL>::MINB))
     k_step_params(KArgs a) {
@@ -2679,7 +2929,10 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
   const int L = fit_layers_of(a, fit);
   if (t >= C::tiles(L)) return;
   const int nb = a.n_pad / 16 / a.n_split, rb0 = split * nb;
-  float* G = a.n_split > 1 ? a.gpart + fit * a.gp_stride + split * a.p_stride : nullptr;
+  // (the unsplit kernel keeps the run-time test: with G a compile-time null
+  // the compiler schedules the Adam epilogue differently and spills, 100-132
+  // B per lane at W = 256 bf16x3)
+  float* G = SK || a.n_split > 1 ? a.gpart + fit * a.gp_stride + split * a.p_stride : nullptr;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n_pad = a.n_pad;
   const float step_size = a.sched[2 * a.epoch], bc2s = a.sched[2 * a.epoch + 1];
@@ -2744,8 +2997,8 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
     sb += __shfl_xor(sb, 1, 64);
     sb += __shfl_xor(sb, 2, 64);
     if (m == 0 && G) {
-      G[j] = sw;
-      G[W + j] = sb;
+      slab_store(a, G + j, sw);
+      slab_store(a, G + W + j, sb);
     } else if (m == 0) {
       float p = P[j], mm = M[j], vv = V[j];
       adam_update(p, mm, vv, sw, step_size, bc2s);
@@ -2755,6 +3008,8 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
       P[W + j] = p; M[W + j] = mm; V[W + j] = vv;
     }
   }
+  if constexpr (SK)
+    if (a.split_fused) split_finish<C, W, D, X3>(a, fit, L, t, lds);
 }
 
 // Split-K second pass: g = Σ_split gpart[split][i] in split order (fixed, so
@@ -2939,6 +3194,11 @@ int validate(int W, int D, int N, int L_max, int epochs) {
 }
 
 constexpr int64_t kMaxSplit = kMaxSplitK;
+int64_t param_tiles(int W, int D, int L, bool small = false);
+int64_t split_ctr_elems(int W, int D, int L_max) {
+  const int64_t t = param_tiles(W, D, L_max, true), u = param_tiles(W, D, L_max, false);
+  return ((t > u ? t : u) + 63) / 64 * 64;
+}
 void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   const int64_t n_pad = ((int64_t)N + kRowPad - 1) / kRowPad * kRowPad;
   s->n_pad = n_pad;
@@ -2956,7 +3216,9 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
   int64_t sp = 1;
   while (sp < kMaxSplit && nb % (4 * sp) == 0 && nb / (2 * sp) >= 4) sp *= 2;
   s->grad_split = sp;
-  s->grad_partial = sp * s->params;
+  // + one int32 arrival counter per parameter tile (the fused split step):
+  // the most tiles any tiling of this shape has, rounded to 64 elements
+  s->grad_partial = sp * s->params + split_ctr_elems(W, D, L_max);
   s->wsplit = xs_size(W, D, L_max);
 }
 
@@ -2965,7 +3227,7 @@ void fill_sizes(int W, int D, int N, int L_max, int epochs, nerfhip_sizes* s) {
 // slices −9 % parameter-kernel time; one wide fit at 8192 (60 tiles) 16
 // slices +9 % (the grid passes 512 there).
 constexpr int64_t kSplitGrid = 512;
-int64_t param_tiles(int W, int D, int L, bool small = false) {   // ParamsCfg<W, D, X3, small>::tiles(L)
+int64_t param_tiles(int W, int D, int L, bool small) {   // ParamsCfg<W, D, X3, small>::tiles(L)
   const int T = small ? 64 : (W < 128 ? W : 128), nt = W / T, TD = D < T ? D : T;
   return (int64_t)L * nt * nt + (int64_t)(D / TD) * nt + W / 64;
 }
@@ -3064,6 +3326,14 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   a.small_tiles = small && a.n_split > 1;
   a.gp_stride = s.grad_partial;
   a.gpart = g->grad_partial;
+  a.ctr_off = s.grad_split * s.params;
+  // NERFHIP_SPLIT_FUSED = 1: the last-arriving slice reduces each tile inside
+  // the parameter kernel (two launches per epoch; bitwise equal, measured
+  // slower: DESIGN.md §12); default the separate k_adam_split pass
+  {
+    const char* e = getenv("NERFHIP_SPLIT_FUSED");
+    a.split_fused = a.n_split > 1 && e && e[0] == '1' ? 1 : 0;
+  }
   a.x3 = g->precision == NERFHIP_PRECISION_BF16X3;
   a.ws_stride = s.wsplit;
   a.wsplit = static_cast<uint16_t*>(g->wsplit);
@@ -3077,7 +3347,7 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   if (const char* e = getenv("NERFHIP_ROWS_LDS_PAD")) a.rows_dyn_lds = pad_kb(e);
   if (const char* e = getenv("NERFHIP_PARAMS_LDS_PAD")) a.params_dyn_lds = pad_kb(e);
 #endif
-#ifdef NERFHIP_STAMPS
+#if defined(NERFHIP_STAMPS) || defined(NERFHIP_EXP_KS_TRACE)
   if (const char* e = getenv("NERFHIP_PSTAMPS"))
     a.pstamps = reinterpret_cast<unsigned long long*>(strtoull(e, nullptr, 0));
 #endif
@@ -3093,21 +3363,26 @@ int launch_rows(const KArgs& a, hipStream_t st) {
   if constexpr (X3 && W >= 128 && D == 128) {
     if (a.rows_ks) {
       const int grid = grid_for(a.n_fits, a.n_pad / 16);
-      // One K-split workgroup per CU, alone (kKsDynLds fills the CU's LDS).
-      // A compile-time forward-only instantiation (MODE = 1, diagnostic
-      // builds only) gives wrong 16-row blocks when two workgroups share a
-      // CU; round 4 showed the compiler's vmcnt placement is
-      // correct under the ISA's in-order model and that only waiting for
-      // every load before the next instruction removes the fault, so its
-      // cause lies below that model.  This single runtime-mode kernel has
-      // measured correct with and without sharing in every probe
-      // (tests/test_gpu_parity.py::test_rows_ks_coresident pins it), and it
-      // still never shares a CU: up to 64 regular workgroups its grid fits
-      // the 256 CUs, up to kKsMaxWorkgroups (128) it takes two rounds (still
-      // faster, rows_ks_for).  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics
-      // only) drops the padding so that two workgroups may share a CU.
+      // One K-split workgroup per CU, alone (kKsDynLds fills the CU's LDS;
+      // the co-residency containment, see kKsDynLds).  This single
+      // runtime-mode kernel has measured correct with and without sharing in
+      // every probe (tests/test_gpu_parity.py::test_rows_ks_coresident pins
+      // it): up to 64 regular workgroups its grid fits the 256 CUs, up to
+      // kKsMaxWorkgroups (128) it takes two rounds (still faster,
+      // rows_ks_for).  NERFHIP_KS_SHARE_CU=1 (tests / diagnostics only)
+      // drops the padding so that two workgroups may share a CU.
       const char* e = getenv("NERFHIP_KS_SHARE_CU");
       unsigned dyn = (e && e[0] == '1') ? 0u : kKsDynLds;
+      // never more than the kernel's own static LDS leaves of the CU's 160 KB
+      // (an over-sized request aborts the queue)
+      static const unsigned dyn_cap = [] {
+        hipFuncAttributes fa;
+        return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_step_rows_ks<W, D, -1>)) ==
+                       hipSuccess
+                   ? 163840u - (unsigned)fa.sharedSizeBytes
+                   : kKsDynLds;
+      }();
+      if (dyn > dyn_cap) dyn = dyn_cap;
 #ifdef NERFHIP_DIAG_ENV
       // diagnostic builds only: an explicit pad (clamped to what fits the CU)
       if (const char* k = getenv("NERFHIP_KS_PAD_KB")) {
@@ -3162,6 +3437,7 @@ int launch_params(const KArgs& a, hipStream_t st) {
       using CS = ParamsCfg<W, D, X3, true>;
       const int grid_s = grid_for(a.n_fits, CS::tiles(a.L_max) * a.n_split);
       hipLaunchKernelGGL((k_step_params<W, D, X3, true>), dim3(grid_s), dim3(CS::THREADS), 0, st, a);
+      if (a.split_fused) return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
       return launch_adam_split<W, D>(a, st);
     }
   }
@@ -3182,9 +3458,14 @@ int launch_params(const KArgs& a, hipStream_t st) {
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
+  if (a.n_split > 1) {
+    hipLaunchKernelGGL((k_step_params<W, D, X3, false, kLayX, true>), dim3(grid),
+                       dim3(ParamsCfg<W, D, X3>::THREADS), a.params_dyn_lds, st, a);
+    if (!a.split_fused) return launch_adam_split<W, D>(a, st);
+    return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+  }
   hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS),
                      a.params_dyn_lds, st, a);
-  if (a.n_split > 1) return launch_adam_split<W, D>(a, st);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
@@ -3305,6 +3586,7 @@ int nerfhip_build_flags(void) {
     defined(NERFHIP_EXP_KS_ALTFIT) || defined(NERFHIP_EXP_KS_LINEAR) ||                      \
     defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
     defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
+    defined(NERFHIP_EXP_KS_TRACE) ||                                                          \
     defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
     defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
     defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \
@@ -3397,6 +3679,12 @@ int prologue(GroupRun& r) {
   const size_t pbytes = (size_t)g->n_fits * r.s.params * sizeof(float);
   if (hipMemsetAsync(g->adam_m, 0, pbytes, r.st) != hipSuccess) return NERFHIP_ERR_LAUNCH;
   if (hipMemsetAsync(g->adam_v, 0, pbytes, r.st) != hipSuccess) return NERFHIP_ERR_LAUNCH;
+  // the fused split step's arrival counters start at 0 (split_finish)
+  if (r.a.split_fused)
+    for (int f = 0; f < g->n_fits; ++f)
+      if (hipMemsetAsync(g->grad_partial + f * r.s.grad_partial + r.a.ctr_off, 0,
+                         (size_t)(r.s.grad_partial - r.a.ctr_off) * sizeof(float), r.st) != hipSuccess)
+        return NERFHIP_ERR_LAUNCH;
   hipLaunchKernelGGL(k_normalize, dim3((g->D + kNormCols - 1) / kNormCols, g->n_fits),
                      dim3(kNormCols * kNormRowGroups), 0, r.st, r.a);
   hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st, r.a);
@@ -3580,7 +3868,7 @@ int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out) {
   out->rows_workgroups = grid_for(a.n_fits, (int)(s.n_pad / rows_per_wg));
   out->params_workgroups =
       grid_for(a.n_fits, (int)param_tiles(g->W, g->D, g->L_max, a.small_tiles != 0) * a.n_split);
-  out->launches_per_epoch = a.n_split > 1 ? 3 : 2;
+  out->launches_per_epoch = a.n_split > 1 && !a.split_fused ? 3 : 2;
   out->reserved = 0;
   return NERFHIP_OK;
 }

@@ -68,7 +68,11 @@ def test_group_sizes(lib, W, D, N, L, E):
     while sp < 16 and nb % (4 * sp) == 0 and nb // (2 * sp) >= 4:
         sp *= 2
     assert s.grad_split == sp == {2048: 16, 192: 2}[n_pad]
-    assert s.grad_partial == sp * s.params
+    # + one int32 arrival counter per parameter tile of the finest tiling (64 x 64
+    # for W >= 128, else W x W; fused split step), rounded to 64 elements
+    t = 64 if W >= 128 else W
+    tiles = L * (W // t) ** 2 + (D // min(D, t)) * (W // t) + W // 64
+    assert s.grad_partial == sp * s.params + (tiles + 63) // 64 * 64
     assert s.wsplit == 6 * (L * W * W + W * D)        # bf16x3 split planes, fwd + transposed
 
 
@@ -104,7 +108,9 @@ def test_group_plan(lib, monkeypatch):
     """nerfhip_group_plan (host only): BASELINE config 2, one medium fit at
     seq 2048 in bf16x3 with the split-K workspace, takes the K-split row kernel
     (one 16-row block per workgroup) and 8 gradient row slices on 64 x 64
-    tiles; a wide fit at 8192 (128 regular workgroups) K-split rows too and
+    tiles, reduced by the k_adam_split pass (three launches per epoch;
+    NERFHIP_SPLIT_FUSED=1 lets the last-arriving slice of each tile reduce it
+    inside the parameter kernel: two); a wide fit at 8192 (128 regular workgroups) K-split rows too and
     128 x 128 tiles x 8 slices; a 40-fit W = 256
     sweep chunk the 32-row kernel (128-row workgroups), fused; a 40-fit
     W = 512 chunk the regular kernels."""
@@ -114,6 +120,10 @@ def test_group_plan(lib, monkeypatch):
     assert (p.rows_variant, p.grad_split, p.rows_workgroups) == (1, 8, 2048 // 16)
     assert p.params_workgroups == 8 * (2 * 16 + 2 * 4 + 256 // 64)     # 44 64x64 tiles x 8 slices
     assert p.launches_per_epoch == 3
+    monkeypatch.setenv("NERFHIP_SPLIT_FUSED", "1")
+    assert _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=1,
+                 grad_partial=1)[1].launches_per_epoch == 2
+    monkeypatch.delenv("NERFHIP_SPLIT_FUSED")
     rc, p = _plan(lib, W=512, D=128, N=8192, n_fits=1, L_max=3, epochs=2000, precision=1,
                   grad_partial=1)
     assert rc == 0 and (p.rows_variant, p.grad_split) == (1, 8)       # 128 regular -> K-split

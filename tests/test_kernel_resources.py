@@ -28,7 +28,7 @@ pytestmark = pytest.mark.skipif(
 KNOWN_SCRATCH = {
     "void k_step_rows<256, 128, true, true>(nerfhip_detail::KArgs)": 120,
     "void k_step_rows<256, 64, true, true>(nerfhip_detail::KArgs)": 120,
-    "void k_step_params<128, 128, true, false, 0>(nerfhip_detail::KArgs)": 12,
+    "void k_step_params<128, 128, true, false, 0, false>(nerfhip_detail::KArgs)": 12,
     # the opt-in 32-row kernel: one 8-byte spill slot at 512 registers
     "void k_step_rows32<256, 128, true>(nerfhip_detail::KArgs)": 8,
 }
@@ -47,15 +47,30 @@ def test_every_step_kernel_present(ks):
     # the fused parameter step in the K-split weight layout (KSX = kLayKs = 1)
     # exists for every K-split width, and in the 32-row layout (kLay32 = 2) at W = 256
     for w in (128, 256, 512):
-        assert f"void k_step_params<{w}, 128, true, false, 1>(nerfhip_detail::KArgs)" in ks
-    assert "void k_step_params<256, 128, true, false, 2>(nerfhip_detail::KArgs)" in ks
+        assert f"void k_step_params<{w}, 128, true, false, 1, false>(nerfhip_detail::KArgs)" in ks
+    assert "void k_step_params<256, 128, true, false, 2, false>(nerfhip_detail::KArgs)" in ks
+    # unsplit and split-K (SK) instantiations of the regular tiles, small tiles split-K only
+    for w in (64, 128, 256, 512):
+        for sk in ("false", "true"):
+            assert f"void k_step_params<{w}, 128, true, false, 0, {sk}>(nerfhip_detail::KArgs)" in ks
+    assert "void k_step_params<256, 128, true, true, 0, true>(nerfhip_detail::KArgs)" in ks
     for t in ("true", "false"):
         assert f"void k_step_rows32<256, 128, {t}>(nerfhip_detail::KArgs)" in ks
 
 
+# the split-K parameter kernels (SK = true, groups under 8 fits): the fused
+# reduction's 16-slab batches spill a little after the tile work (cold path,
+# once per tile and epoch; the tile loops themselves stay in registers)
+SPLIT_SCRATCH_MAX = 160
+
+
 def test_no_unexpected_scratch(ks):
+    def allowed(n):
+        if n.startswith("void k_step_params<") and n.endswith(", true>(nerfhip_detail::KArgs)"):
+            return max(KNOWN_SCRATCH.get(n, 0), SPLIT_SCRATCH_MAX)
+        return KNOWN_SCRATCH.get(n, 0)
     bad = {n: v["private_segment_fixed_size"] for n, v in ks.items()
-           if v.get("private_segment_fixed_size", 0) > KNOWN_SCRATCH.get(n, 0)}
+           if v.get("private_segment_fixed_size", 0) > allowed(n)}
     assert not bad, bad
 
 

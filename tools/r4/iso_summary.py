@@ -40,7 +40,7 @@ def main():
     kind = ev["kernel"].split("<")[0]
     x3 = "true" if ev["precision"] == "bf16x3" else "false"
     pat = re.compile(rf"{kind}<{W}, 128, {x3}, (true|false)(, false)*>" if kind == "k_step_rows"
-                     else rf"{kind}<{W}, 128, {x3}, false, false(, \d+)?>")
+                     else rf"{kind}<{W}, 128, {x3}, false(, false)?(, \d+)?(, false)?>")
     # the 32-row training kernel (k_step_rows32<W, 128, TRAIN>) stands in for
     # k_step_rows when the library selects it
     pat32 = re.compile(rf"k_step_rows32<{W}, 128, true>")
