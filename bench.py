@@ -25,7 +25,7 @@ Also reported (rank 0):
                 of its width timed alone (hipEvents on 25 launches of a
                 101-epoch run right after the timed region, the cold first
                 launch excluded; the same leg under rocprofv3 is committed in
-                profiles/r04, tools/r4/iso_prof.sh); `frac_concurrent` is the same
+                profiles/r05, tools/r4/iso_prof.sh); `frac_concurrent` is the same
                 kernel's launches inside the timed sweep, where ~7 group
                 streams share the GPU; `job_frac` is the whole sweep's
                 algorithmic rate;
@@ -241,8 +241,8 @@ ISO_EPOCHS = 101   # isolated leg: 25 timed launches (every 4th epoch from epoch
 # the committed rocprofv3 summary of exactly that leg (tools/r4/iso_prof.sh runs
 # tools/r4/isokernel.py, which calls isolated_kernel below, under
 # rocprofv3 --kernel-trace --stats, and its PMC passes)
-ISO_PROFILE = "profiles/r04/rocprof_kernel_stats_isolated_rows256.csv"
-ISO_PMC = ROOT / "profiles" / "r04" / "pmc_isolated_rows256.json"
+ISO_PROFILE = "profiles/r05/rocprof_kernel_stats_isolated_rows256.csv"
+ISO_PMC = ROOT / "profiles" / "r05" / "pmc_isolated_rows256.json"
 
 
 def lib_sha16() -> str:
@@ -500,7 +500,7 @@ def main() -> None:
                     "traffic_detail": iso_pmc,
                     "traffic_source": "rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of the "
                                       "same isolated group (tools/r4/iso_prof.sh, "
-                                      "profiles/r04/pmc_isolated_rows256.json)",
+                                      "profiles/r05/pmc_isolated_rows256.json)",
                     "mfma_busy": iso_pmc and iso_pmc.get("mfma_busy"),
                     "algorithmic_bytes": alg_bytes,
                     "algorithmic_bytes_kind": "SURVEY.md §8d per fit-epoch 4·N·D target + 24·P "

@@ -38,6 +38,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <math.h>
 #include <type_traits>
@@ -541,8 +542,11 @@ __host__ __device__ inline int64_t n_params(int W, int D, int L) {
 // arriving workgroup a write-back of its XCD's whole dirty L2
 // (cdna_hip_programming.md, in-launch split-K); k_adam_split's slabs cross a
 // kernel boundary and stay plain.
-__device__ __forceinline__ void slab_store(const nerfhip_detail::KArgs& a, float* p, float v) {
-  if (a.split_fused) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// (WT: compile-time, the fused instantiation only — a run-time select put
+// exec-masked branches around the slab stores of every split-K launch)
+template <bool WT>
+__device__ __forceinline__ void slab_store(float* p, float v) {
+  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
 
@@ -2366,7 +2370,7 @@ template <bool X3> __device__ __forceinline__ int stage_slot(int i) {
   return (i & ~63) | (f << 2) | (l & 3);
 }
 
-template <int TJ, int TK, int NW>
+template <int TJ, int TK, int NW, bool WT = false>
 __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict__ A, int FA,
                                         const float* __restrict__ B, int FB, int j0, int k0,
                                         int rb0, int n_blocks, float* G,
@@ -2483,7 +2487,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
           const int j = jrow0 + qq + 8 * qb + 4 * h;
           const int64_t idx = pw + (int64_t)j * a.W + kcol;
           if (G) {
-            slab_store(a, G + idx, acc[x][y][qb * 4 + qq]);
+            slab_store<WT>(G + idx, acc[x][y][qb * 4 + qq]);
             continue;
           }
           float p = P[idx], mm = M[idx], vv = V[idx];
@@ -2501,7 +2505,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
       if (h == 0) {
         const int64_t idx = pb + j0 + wj * (TJ / 2) + 32 * x + lr;
         if (G) {
-          slab_store(a, G + idx, s);
+          slab_store<WT>(G + idx, s);
           continue;
         }
         float p = P[idx], mm = M[idx], vv = V[idx];
@@ -2526,7 +2530,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // transposed fp32 copy, both split copies of the weights for the row kernel.
 constexpr int kFx = 24;
 
-template <int TJ, int TK, int NW, int WW, int OD, int KSX>
+template <int TJ, int TK, int NW, int WW, int OD, int KSX, bool WT = false>
 __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
                                            const float* __restrict__ B, int FB, int j0, int k0,
                                            int rb0, int n_blocks, float* G, float* P, float* M,
@@ -2681,7 +2685,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           const int64_t idx = pw + (int64_t)j * W + kcol;
           const float gsum = hi[x][y][qb * 4 + qq] + lo[x][y][qb * 4 + qq];
           if (G) {
-            slab_store(a, G + idx, gsum);
+            slab_store<WT>(G + idx, gsum);
             continue;
           }
           float p = P[idx], mm = M[idx], vv = V[idx];
@@ -2715,7 +2719,7 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
       if ((tid & 3) == 0 && tid + NTH * m < NA4) {
         const int64_t idx = pb + j0 + (stage_slot<true>(tid + NTH * m) >> 2);
         if (G) {
-          slab_store(a, G + idx, s);
+          slab_store<WT>(G + idx, s);
         } else {
           float p = P[idx], mm = M[idx], vv = V[idx];
           adam_update(p, mm, vv, s, step_size, bc2s);
@@ -2911,9 +2915,11 @@ template <int W, int D, bool X3, bool SMALL = false> struct ParamsCfg {
   __host__ __device__ static int tiles(int L) { return L * TH + TF + T0; }
 };
 
-// SK: the split-K instantiation (launched only for n_split > 1: partial slabs,
-// and the fused reduction); the unsplit one has no slab path at all.
-template <int W, int D, bool X3, bool SMALL = false, int KSX = kLayX, bool SK = SMALL>
+// SK: the fused split-K instantiation (NERFHIP_SPLIT_FUSED=1: write-through
+// slabs and the in-kernel reduction).  Every other launch — unsplit, or
+// split-K with the k_adam_split pass — runs SK = false, whose slab path is
+// the run-time `G` test alone.
+template <int W, int D, bool X3, bool SMALL = false, int KSX = kLayX, bool SK = false>
 __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
                                   (ParamsCfg<W, D, X3, SMALL>::MINB))
     k_step_params(KArgs a) {
@@ -2952,14 +2958,14 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
     const int layer = t / C::TH + 1, u = t % C::TH;
     const int64_t pw = off_hidden_w(W, layer);
     if constexpr (X3)
-      dw_tile_x3<C::T, C::TK, C::NW, W, W, KSX>(a, SZ + (int64_t)layer * WN, W,
+      dw_tile_x3<C::T, C::TK, C::NW, W, W, KSX, SK>(a, SZ + (int64_t)layer * WN, W,
                                      SH + (int64_t)(layer - 1) * WN, W, (u / C::NTK) * C::T,
                                      (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
                                      pw + (int64_t)W * W, xs_mat(W, D, L, false, layer),
                                      xs_mat(W, D, L, true, layer), W, (u % C::NTK) == 0,
                                      step_size, bc2s, lds);
     else
-      dw_tile<C::T, C::T, C::NW>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN,
+      dw_tile<C::T, C::T, C::NW, SK>(a, SZ + (int64_t)layer * WN, W, SH + (int64_t)(layer - 1) * WN,
                                  W, (u / C::NTK) * C::T, (u % C::NTK) * C::T, rb0, nb, G, P, M, V,
                                  PT, pw, pw + (int64_t)W * W, (int64_t)(layer - 1) * W * W, W,
                                  (u % C::NTK) == 0, step_size, bc2s, lds);
@@ -2967,13 +2973,13 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
     const int u = t - L * C::TH;
     const int64_t pw = off_final_w(W, L);
     if constexpr (X3)
-      dw_tile_x3<C::TD, C::TK, C::NW, W, D, KSX>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
+      dw_tile_x3<C::TD, C::TK, C::NW, W, D, KSX, SK>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
                                       (u % C::NTK) * C::TK, rb0, nb, G, P, M, V, XS, pw,
                                       pw + (int64_t)W * D, xs_mat(W, D, L, false, L + 1),
                                       xs_mat(W, D, L, true, L + 1), D, (u % C::NTK) == 0,
                                       step_size, bc2s, lds);
     else
-      dw_tile<C::TD, C::T, C::NW>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
+      dw_tile<C::TD, C::T, C::NW, SK>(a, SG, D, SH + (int64_t)L * WN, W, (u / C::NTK) * C::TD,
                                   (u % C::NTK) * C::T, rb0, nb, G, P, M, V, PT, pw,
                                   pw + (int64_t)W * D, (int64_t)L * W * W, D, (u % C::NTK) == 0,
                                   step_size, bc2s, lds);
@@ -2997,8 +3003,8 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
     sb += __shfl_xor(sb, 1, 64);
     sb += __shfl_xor(sb, 2, 64);
     if (m == 0 && G) {
-      slab_store(a, G + j, sw);
-      slab_store(a, G + W + j, sb);
+      slab_store<SK>(G + j, sw);
+      slab_store<SK>(G + W + j, sb);
     } else if (m == 0) {
       float p = P[j], mm = M[j], vv = V[j];
       adam_update(p, mm, vv, sw, step_size, bc2s);
@@ -3436,8 +3442,12 @@ int launch_params(const KArgs& a, hipStream_t st) {
     if (a.small_tiles) {
       using CS = ParamsCfg<W, D, X3, true>;
       const int grid_s = grid_for(a.n_fits, CS::tiles(a.L_max) * a.n_split);
+      if (a.split_fused) {
+        hipLaunchKernelGGL((k_step_params<W, D, X3, true, kLayX, true>), dim3(grid_s),
+                           dim3(CS::THREADS), 0, st, a);
+        return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
+      }
       hipLaunchKernelGGL((k_step_params<W, D, X3, true>), dim3(grid_s), dim3(CS::THREADS), 0, st, a);
-      if (a.split_fused) return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
       return launch_adam_split<W, D>(a, st);
     }
   }
@@ -3458,14 +3468,14 @@ int launch_params(const KArgs& a, hipStream_t st) {
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
-  if (a.n_split > 1) {
+  if (a.split_fused) {
     hipLaunchKernelGGL((k_step_params<W, D, X3, false, kLayX, true>), dim3(grid),
                        dim3(ParamsCfg<W, D, X3>::THREADS), a.params_dyn_lds, st, a);
-    if (!a.split_fused) return launch_adam_split<W, D>(a, st);
     return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
   }
   hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS),
                      a.params_dyn_lds, st, a);
+  if (a.n_split > 1) return launch_adam_split<W, D>(a, st);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
@@ -3691,6 +3701,25 @@ int prologue(GroupRun& r) {
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
+// NERFHIP_SYNC_CHECK=1 (debugging): synchronise after every launch and name
+// the failing step on stderr (group shape, epoch, which kernel)
+bool sync_check_on() {
+  static const bool on = [] {
+    const char* e = getenv("NERFHIP_SYNC_CHECK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+int sync_check(const GroupRun& r, int e, const char* what, int rc) {
+  if (rc != NERFHIP_OK || !sync_check_on()) return rc;
+  const hipError_t err = hipStreamSynchronize(r.st);
+  if (err == hipSuccess) return rc;
+  fprintf(stderr, "nerfhip: %s failed: W=%d D=%d N=%d n_fits=%d L_max=%d epoch=%d split=%d rows_ks=%d: %s\n",
+          what, r.g->W, r.g->D, r.g->N, r.g->n_fits, r.g->L_max, e, r.a.n_split, r.a.rows_ks,
+          hipGetErrorString(err));
+  return NERFHIP_ERR_LAUNCH;
+}
+
 int epoch_step(GroupRun& r, int e, hipEvent_t* ev /* 3 or NULL */) {
   KArgs& a = r.a;
   a.epoch = e;
@@ -3701,14 +3730,14 @@ int epoch_step(GroupRun& r, int e, hipEvent_t* ev /* 3 or NULL */) {
     a.y_stride = r.probe_stride;
   }
   if (ev) (void)hipEventRecord(ev[0], r.st);
-  int rc = r.rows(a, r.st);
+  int rc = sync_check(r, e, "row step", r.rows(a, r.st));
 #ifdef NERFHIP_DIAG_ROWS_TWICE
   // diagnostic build only: the row step again (same inputs, same outputs) with
   // its weight planes now resident in L2 — how much of it is cold weight reads
   if (rc == NERFHIP_OK) rc = r.rows(a, r.st);
 #endif
   if (ev) (void)hipEventRecord(ev[1], r.st);
-  if (rc == NERFHIP_OK) rc = r.params(a, r.st);
+  if (rc == NERFHIP_OK) rc = sync_check(r, e, "parameter step", r.params(a, r.st));
   if (ev) (void)hipEventRecord(ev[2], r.st);
   return rc;
 }

@@ -432,16 +432,19 @@ def test_synthetic_spawn_pool_bitwise_and_leaves_nothing(monkeypatch):
     monkeypatch.setattr(synthetic, "_hip_untouched", lambda: False)
     monkeypatch.setattr(synthetic, "POOL_MIN_ROWS", 0)
     monkeypatch.setattr(synthetic, "_threads", lambda: 2)
+    from multiprocessing import resource_tracker
     pairs = [(0, 0), (3, 1), (5, 2)]
     before = set(glob.glob("/dev/shm/nerf_synth_*"))
+    # (another test of this session may already have started the process's
+    # tracker: this call must not start one, and must not restart it)
+    tracker = getattr(resource_tracker._resource_tracker, "_pid", None)
     got = synthetic.kv_slices(pairs, seq_len=256, num_layers=8, num_kv_heads=4)
     for (l, h), (k, v) in zip(pairs, got):
         k0, v0 = kv_slice(l, h, seq_len=256, num_layers=8, num_kv_heads=4)
         assert torch.equal(k, k0) and torch.equal(v, v0)
     assert mp.active_children() == []
     assert set(glob.glob("/dev/shm/nerf_synth_*")) == before
-    from multiprocessing import resource_tracker
-    assert getattr(resource_tracker._resource_tracker, "_pid", None) is None
+    assert getattr(resource_tracker._resource_tracker, "_pid", None) == tracker
 
 
 def test_init_replay_self_check(monkeypatch):
