@@ -424,6 +424,20 @@ def plan_groups(specs: list, device: int) -> list:
     return sorted(parts, key=lambda dm: -sum(costs[i] for i in dm[1]))
 
 
+def split_allowed(n_groups: int) -> bool:
+    """Whether small groups may take the split-K weight-gradient path.
+
+    Only when the job trains ONE group on its device (a lone fit — BASELINE
+    configs 2 and 5 — or a few fits of one shape).  With several groups
+    training concurrently on one GPU (the 8-rank shares: 5-fit W = 64 / 128
+    split groups beside W = 256 / 512 groups), round 5 saw intermittent
+    illegal-address faults that never appeared with the split path off, with
+    per-launch synchronisation, or in a lone group; those
+    groups train unsplit until the cause is found.  NERFHIP_SPLIT_CONCURRENT=1
+    allows it anyway (diagnostics)."""
+    return n_groups <= 1 or os.environ.get("NERFHIP_SPLIT_CONCURRENT") == "1"
+
+
 class FitJob:
     """A set of fits with every input already resident on its device.
 
@@ -445,6 +459,7 @@ class FitJob:
         self.specs = specs
         self.epochs = epochs
         self.plan = plan_groups(specs, self.device)
+        split = split and split_allowed(len(self.plan))
         # (diagnostic: NERFHIP_PRIO_HEAVY=1 gives the heaviest group, the
         # sweep's critical path, a high-priority stream)
         heavy = os.environ.get("NERFHIP_PRIO_HEAVY", "0") == "1"
@@ -591,8 +606,8 @@ class StreamingJob:
     def _run(self, gi: int) -> None:
         try:
             d, members = self.plan[gi]
-            g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d, True,
-                       self.precision)
+            g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d,
+                       split_allowed(len(self.plan)), self.precision)
             self.groups[gi] = g
             g.ev_start.record(g.stream)
             desc = (_native.NerfhipGroup * 1)(g.desc)
