@@ -50,7 +50,9 @@ KIND_FLAGS = {1: [], 2: ["-fno-slp-vectorize"]}
 # accumulators in VGPRs; -amdgpu-mfma-vgpr-form makes the compiler select the
 # VGPR form of the MFMA destination (without it the accumulators go to AGPRs
 # too, and 192 AGPRs of B plus 32 of accumulators do not fit beside them).
-R32_UNITS = [(6, 3, ["-mllvm", "-amdgpu-mfma-vgpr-form=1"])]
+# Also without SLP vectorisation, like the parameter kernels: 2-3 % faster
+# (profiles/r05/ab_r32_variants.log, v_r32noslp).
+R32_UNITS = [(6, 3, ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"])]
 
 
 def build(force: bool = False, verbose: bool = True) -> Path:

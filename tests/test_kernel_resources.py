@@ -29,8 +29,8 @@ KNOWN_SCRATCH = {
     "void k_step_rows<256, 128, true, true>(nerfhip_detail::KArgs)": 120,
     "void k_step_rows<256, 64, true, true>(nerfhip_detail::KArgs)": 120,
     "void k_step_params<128, 128, true, false, 0, false>(nerfhip_detail::KArgs)": 12,
-    # the opt-in 32-row kernel: one 8-byte spill slot at 512 registers
-    "void k_step_rows32<256, 128, true>(nerfhip_detail::KArgs)": 8,
+    # the opt-in 32-row kernel: a few spill slots at 512 registers
+    "void k_step_rows32<256, 128, true>(nerfhip_detail::KArgs)": 20,
 }
 
 
