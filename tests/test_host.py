@@ -466,3 +466,44 @@ def test_init_replay_self_check(monkeypatch):
     torch.manual_seed(3)
     b = siren.init_flat(cfg, 64)
     assert torch.equal(a, b)
+
+
+def test_split_allowed_only_for_one_group(monkeypatch):
+    """The split-K weight-gradient path is given only to jobs that train one
+    group on the device (engine.split_allowed; DESIGN.md §12: an open fault
+    with concurrent split groups); NERFHIP_SPLIT_CONCURRENT=1 overrides."""
+    monkeypatch.delenv("NERFHIP_SPLIT_CONCURRENT", raising=False)
+    assert engine.split_allowed(1) and engine.split_allowed(0)
+    assert not engine.split_allowed(2) and not engine.split_allowed(4)
+    monkeypatch.setenv("NERFHIP_SPLIT_CONCURRENT", "1")
+    assert engine.split_allowed(4)
+
+
+def test_ks_lds_hb_checker_on_synthetic_traces():
+    """tools/r5/ks_lds_hb.py's happens-before rule on hand-made traces: a
+    cross-wave write→read or read→overwrite of one LDS address inside one
+    barrier interval is a race; the same pair across a barrier, or within one
+    wave, is not; and ignoring the barriers exposes the separated pairs."""
+    import importlib.util
+    import numpy as np
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    spec = importlib.util.spec_from_file_location("ks_lds_hb", root / "tools/r5/ks_lds_hb.py")
+    hb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(hb)
+
+    def trace(events):   # events: {wave: [(bc, rw, addr), ...]} -> [4][MAXEV][64]
+        tr = np.full((4, hb.MAXEV, 64), 0xFFFFFFFF, dtype=np.uint32)
+        for w, evs in events.items():
+            for n, (bc, rw, addr) in enumerate(evs):
+                tr[w, n, :] = (bc << 18) | (rw << 17) | addr
+        return tr
+
+    clean = trace({0: [(0, 1, 64), (1, 0, 128)], 1: [(1, 0, 64), (0, 1, 128)],
+                   2: [(0, 1, 256), (0, 0, 256)], 3: [(2, 1, 64)]})
+    r = hb.check(clean)
+    assert r["races"] == 0 and r["events_per_wave"] == [2, 2, 2, 1]
+    assert hb.check(clean, bc_override=True)["races"] > 0
+    raw = trace({0: [(3, 1, 512)], 1: [(3, 0, 512)]})          # write -> read, same interval
+    war = trace({0: [(5, 0, 768)], 2: [(5, 1, 768)]})          # read -> overwrite
+    assert hb.check(raw)["races"] == 1 and hb.check(war)["races"] == 1
