@@ -253,6 +253,19 @@ def lib_sha16() -> str:
     return hashlib.sha256(Path(os.environ.get("NERFHIP_LIB", _build.LIB)).read_bytes()).hexdigest()[:16]
 
 
+def committed_pmc(path: Path, key: str, cur_lib: str):
+    """The committed PMC summary of `key` (tools/r4/iso_summary.py), or None;
+    a summary measured on another build of the library comes back as a stale
+    marker without its figures (its bytes / MFMA busy would describe other
+    code)."""
+    if not path.exists():
+        return None
+    pmc = json.loads(path.read_text()).get(key)
+    if pmc and pmc.get("lib_sha16") != cur_lib:
+        return {"stale": True, "pmc_lib_sha16": pmc.get("lib_sha16"), "lib_sha16": cur_lib}
+    return pmc
+
+
 def heaviest_group(specs, width: int, device: int = 0) -> list:
     """Indices (into `specs`) of the engine's heaviest group of hidden width
     `width`, exactly as engine.plan_groups chunks the job (the sweep's W = 256
@@ -473,14 +486,7 @@ def main() -> None:
             iso = isolated_kernel([my_specs[i] for i in gsel], kname, g_flops,
                                   args.precision, peak, local)
             iso["fits"] = len(gsel)
-            iso_pmc = None
-            if ISO_PMC.exists():
-                iso_pmc = json.loads(ISO_PMC.read_text()).get(f"{kname}[{args.precision}]")
-            pmc_lib = iso_pmc and iso_pmc.get("lib_sha16")
-            cur_lib = lib_sha16()
-            if iso_pmc and pmc_lib != cur_lib:
-                # the committed counters describe another build of the kernel
-                iso_pmc = {"stale": True, "pmc_lib_sha16": pmc_lib, "lib_sha16": cur_lib}
+            iso_pmc = committed_pmc(ISO_PMC, f"{kname}[{args.precision}]", lib_sha16())
             iso_bytes = iso_pmc and iso_pmc.get("bytes")
             hbm_iso = iso_bytes and iso_bytes / (iso["avg_launch_ms"] * 1e-3) / 1e9
             alg_bytes = sum(4 * N * 128 + 24 * c.num_parameters(128) for c in gcf)

@@ -234,3 +234,25 @@ def test_bench_raises_hw_queues(given, keep, want):
                        timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().splitlines()[-1] == want
+
+
+def test_bench_pmc_figures_only_for_the_measured_library(tmp_path):
+    """bench.committed_pmc reports a committed PMC summary only for the
+    library build it was measured on (the summary's lib_sha16); for any other
+    build it returns a stale marker without bytes or MFMA busy."""
+    import json
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root))
+    import bench
+    f = tmp_path / "pmc.json"
+    f.write_text(json.dumps({"k[bf16x3]": {"bytes": 5.0, "mfma_busy": 0.3, "lib_sha16": "aa"}}))
+    assert bench.committed_pmc(f, "k[bf16x3]", "aa")["bytes"] == 5.0
+    stale = bench.committed_pmc(f, "k[bf16x3]", "bb")
+    assert stale["stale"] and "bytes" not in stale and stale["pmc_lib_sha16"] == "aa"
+    assert bench.committed_pmc(f, "other", "aa") is None
+    assert bench.committed_pmc(tmp_path / "missing.json", "k[bf16x3]", "aa") is None
+    # the committed round-5 summary names the in-tree library when it is current
+    real = json.loads((root / "profiles/r05/pmc_isolated_rows256.json").read_text())
+    assert all("lib_sha16" in v for v in real.values())
