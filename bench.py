@@ -590,5 +590,19 @@ def main() -> None:
         dist.destroy_process_group()
 
 
+def report_children() -> None:
+    """Every process this one started that is still alive, on stderr (the
+    driver's record showed one process outliving bench.py)."""
+    try:
+        import psutil
+        kids = psutil.Process().children(recursive=True)
+    except Exception as e:                              # psutil missing / no /proc
+        progress(f"children at exit: unknown ({e})")
+        return
+    progress(f"children at exit: {len(kids)}" + "".join(
+        f"; pid {k.pid} {' '.join(k.cmdline())[:160]}" for k in kids if k.is_running()))
+
+
 if __name__ == "__main__":
     main()
+    report_children()

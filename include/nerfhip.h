@@ -117,7 +117,10 @@ typedef struct nerfhip_group {
                                  fixed-order sum + Adam): a small group
                                  otherwise fills only a few workgroups
                                  (nerfhip_group_plan reports the slices).
-                                 Deterministic; slices and tiles depend on the group shape only. */
+                                 Deterministic; slices and tiles depend on the
+                                 group shape only — not on n_groups or on what
+                                 else trains on the device (round 6 lifted the
+                                 round-5 single-group rule). */
   void* wsplit;               /* [n] uint16 workspace, BF16X3 only (else NULL):
                                  every weight as exact bf16 split planes, in
                                  the forward and the transposed orientation,
@@ -169,7 +172,8 @@ typedef enum nerfhip_rows_variant {
   NERFHIP_ROWS_KSPLIT = 1,    /* k_step_rows_ks: four waves split every GEMM's k over one
                                  16-row block (small bf16x3 groups, W >= 128, D = 128)   */
   NERFHIP_ROWS_32 = 2         /* k_step_rows32: 128-row workgroups, one wave per 32 rows,
-                                 32x32x16 MFMAs (bf16x3, W = 256, D = 128, n_pad % 128 = 0) */
+                                 32x32x16 MFMAs (bf16x3, W = 256, D = 128, n_pad % 128 = 0;
+                                 NERFHIP_VARIANTS builds only) */
 } nerfhip_rows_variant;
 
 typedef struct nerfhip_plan {
@@ -186,10 +190,14 @@ int nerfhip_group_plan(const nerfhip_group* g, nerfhip_plan* out);
 /* Diagnostic compile-time switches this library was built with (0 for a
  * product build): bit 0 any NERFHIP_EXP_* timing/diagnostic macro (such
  * builds may compute wrong results on purpose), bit 1 NERFHIP_STAMPS
- * (in-kernel timestamps), bit 2 NERFHIP_DIAG_* (altered launch sequence). */
+ * (in-kernel timestamps), bit 2 NERFHIP_DIAG_* (altered launch sequence),
+ * bit 3 NERFHIP_VARIANTS (the opt-in kernels that measured slower than the
+ * defaults: the 32-row row kernel, NERFHIP_ROWS32=1, and the fused split-K
+ * reduction, NERFHIP_SPLIT_FUSED=1; a product build ignores both switches). */
 #define NERFHIP_BUILD_EXP 1
 #define NERFHIP_BUILD_STAMPS 2
 #define NERFHIP_BUILD_DIAG 4
+#define NERFHIP_BUILD_VARIANTS 8
 int nerfhip_build_flags(void);
 
 /* ------------------------------------------------------------------------

@@ -20,7 +20,7 @@ LIB_DIR = PKG / "_lib"
 LIB = LIB_DIR / "libnerfhip.so"
 SOURCES = [CSRC / "nerfhip.hip", CSRC / "nerfhip_svd.hip", CSRC / "nerfhip_analysis.hip",
            CSRC / "nerfhip_rng.cpp"]
-HEADERS = [INCLUDE / "nerfhip.h"]
+HEADERS = [INCLUDE / "nerfhip.h", CSRC / "nerfhip_layout.h"]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("NERFHIP_ARCH", "gfx950")
@@ -52,7 +52,18 @@ KIND_FLAGS = {1: [], 2: ["-fno-slp-vectorize"]}
 # too, and 192 AGPRs of B plus 32 of accumulators do not fit beside them).
 # Also without SLP vectorisation, like the parameter kernels: 2-3 % faster
 # (profiles/r05/ab_r32_variants.log, v_r32noslp).
+# The unit exists only in NERFHIP_VARIANTS builds (tools/build_variant.py with
+# -DNERFHIP_VARIANTS): the kernel measured slower than the 16-row one
+#  and is not part of the product library.
 R32_UNITS = [(6, 3, ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"])]
+
+
+def units(defines=()) -> list:
+    """(part, kind, flags) of every translation unit of nerfhip.hip; the
+    32-row unit only when `defines` carries -DNERFHIP_VARIANTS."""
+    out = [(0, 0, [])] + [(part, kind, KIND_FLAGS[kind]) for part in range(1, N_PARTS)
+                          for kind in KIND_FLAGS]
+    return out + (R32_UNITS if "-DNERFHIP_VARIANTS" in defines else [])
 
 
 def build(force: bool = False, verbose: bool = True) -> Path:
@@ -67,9 +78,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function", "-I", str(INCLUDE)]
     objs, procs = [], []
-    units = ([(0, 0, [])] + [(part, kind, KIND_FLAGS[kind]) for part in range(1, N_PARTS)
-                             for kind in KIND_FLAGS] + R32_UNITS)
-    for part, kind, flags in units:
+    for part, kind, flags in units():
         obj = obj_dir / (f"nerfhip_p{part}.o" if kind == 0 else f"nerfhip_p{part}k{kind}.o")
         cmd = base + flags + [f"-DNERFHIP_PART={part}",
                                                  f"-DNERFHIP_KIND={kind}", "-c", str(SOURCES[0]),

@@ -57,11 +57,12 @@ class FitOutput:
     final_mse: float              # siren.py:123
     probes: list = field(default_factory=list)  # (epoch, norm_mse, real_mse, cos)
     # the reference's quantity (siren.py:96,117) is the wall clock of the epoch
-    # loop that trained this fit, and its sum over a sequential sweep is the
-    # sweep's training time.  Fits that train concurrently have no loop of their
-    # own, so each gets the job's wall clock x its share of the job's FLOPs
-    # (SURVEY §8d model): a lone fit (fit_siren) gets its own loop time, and the
-    # sum over a job's fits is the job's wall clock, as in the reference
+    # loop that trained this fit.  Here a fit trains inside its group's launches
+    # (all fits of a group step together, one kernel pair per epoch), so the
+    # measured interval of ITS training is the group's: hipEvents on the
+    # group's stream before its first and after its last launch (device clock).
+    # A lone fit (fit_siren) gets exactly its own loop time; fits of concurrent
+    # groups overlap, so a sweep's records sum to more than its wall clock.
     train_time_seconds: float = 0.0
     flop_share_seconds: float = 0.0   # group time x this fit's share of its group's FLOPs
     group_seconds: float = 0.0
@@ -120,6 +121,23 @@ SPLIT_MIN_TILES = 128
 # its own stream's queue depth only) instead of one thread interleaving the
 # groups epoch by epoch
 LAUNCH_THREADS = os.environ.get("NERFHIP_LAUNCH_THREADS", "0") == "1"
+
+
+def wants_split(n_fits: int, W: int, D: int, L_max: int, grad_split: int) -> bool:
+    """Whether a group of this shape gets the split-K workspace (grad_partial):
+    under SPLIT_MAX_FITS fits, with a fused parameter grid under
+    SPLIT_MIN_TILES workgroups, and row slices available (grad_split > 1).
+    A function of the group's own shape only — not of how many other groups
+    train beside it on the device (round 5's engine.split_allowed, removed in
+    round 6: DESIGN.md §13) — so a fit's numerics are the same in every job
+    that forms the same group (farm worker or single process).
+    NERFHIP_SPLIT_MAX_FITS caps the group size (0 = never; any setting also
+    lifts the SPLIT_MIN_TILES condition, diagnostics)."""
+    env = os.environ.get("NERFHIP_SPLIT_MAX_FITS")
+    split_max = int(env) if env is not None else SPLIT_MAX_FITS
+    small = n_fits * param_tiles(W, D, L_max) < SPLIT_MIN_TILES
+    return (n_fits < min(split_max, SPLIT_MAX_FITS) and grad_split > 1
+            and (small or env is not None))
 
 
 def param_tiles(W: int, D: int, L: int) -> int:
@@ -223,11 +241,8 @@ class _Group:
         self.row_sq = torch.empty(n, n_pad, **f32)
         # groups of < SPLIT_MAX_FITS fits reduce the weight gradient in row
         # slices (nerfhip.h grad_partial); the sweep's groups never need it
-        split_max = int(os.environ.get("NERFHIP_SPLIT_MAX_FITS", SPLIT_MAX_FITS))
-        small = n * param_tiles(self.W, self.D, self.L_max) < SPLIT_MIN_TILES
         self.grad_partial = torch.empty(n, int(s.grad_partial), **f32) \
-            if (split and n < min(split_max, SPLIT_MAX_FITS) and s.grad_split > 1
-                and (small or "NERFHIP_SPLIT_MAX_FITS" in os.environ)) else None
+            if split and wants_split(n, self.W, self.D, self.L_max, int(s.grad_split)) else None
         self.wsplit = torch.empty(n, int(s.wsplit), dtype=torch.int16, device=dev) \
             if precision == "bf16x3" else None
         if self.n_probe:
@@ -261,7 +276,7 @@ class _Group:
                 "rows_workgroups": p.rows_workgroups, "params_workgroups": p.params_workgroups,
                 "launches_per_epoch": p.launches_per_epoch}
 
-    def outputs(self, specs, group_seconds, job_seconds=None, job_flops=None):
+    def outputs(self, specs, group_seconds):
         N, D, n = self.N, self.D, self.n
         numel = float(N * D)
         E = self.epochs
@@ -296,8 +311,7 @@ class _Group:
                 target_std=std[k].view(1, D).clone(),
                 losses=[float(x) for x in losses[k]], row_cos=row_cos[k].copy(),
                 row_mse=row_mse[k].copy(), final_mse=float(final_mse[k]), probes=probes,
-                train_time_seconds=(job_seconds * flops[k] / job_flops
-                                    if job_seconds is not None and job_flops else group_seconds),
+                train_time_seconds=group_seconds,
                 flop_share_seconds=group_seconds * flops[k] / tot,
                 group_seconds=group_seconds, device=self.device, plan=dict(plan)))
         return outs
@@ -371,7 +385,10 @@ def plan_groups(specs: list, device: int) -> list:
     regroup the same sums, so a fit's result can differ at the rounding level
     (|Δcos| well under 1e-4) with the chunking or the farm partition that put
     it in a smaller or larger group; `test_group_chunks_row_variant_rounding`
-    pins that, `test_group_chunks_equal_one_group` the bitwise case.
+    pins that, `test_group_chunks_equal_one_group` the bitwise case.  Both
+    choices depend on the group's shape alone (wants_split, rows_ks_for), not
+    on the other groups of the job: the same group trains bitwise the same in
+    a farm worker and in a single process (test_farm_lone_split_fits_bitwise).
     Records are written in the reference's order whatever the grouping:
     outputs are indexed by spec."""
     costs = [fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config, 1)
@@ -424,20 +441,6 @@ def plan_groups(specs: list, device: int) -> list:
     return sorted(parts, key=lambda dm: -sum(costs[i] for i in dm[1]))
 
 
-def split_allowed(n_groups: int) -> bool:
-    """Whether small groups may take the split-K weight-gradient path.
-
-    Only when the job trains ONE group on its device (a lone fit — BASELINE
-    configs 2 and 5 — or a few fits of one shape).  With several groups
-    training concurrently on one GPU (the 8-rank shares: 5-fit W = 64 / 128
-    split groups beside W = 256 / 512 groups), round 5 saw intermittent
-    illegal-address faults that never appeared with the split path off, with
-    per-launch synchronisation, or in a lone group; those
-    groups train unsplit until the cause is found.  NERFHIP_SPLIT_CONCURRENT=1
-    allows it anyway (diagnostics)."""
-    return n_groups <= 1 or os.environ.get("NERFHIP_SPLIT_CONCURRENT") == "1"
-
-
 class FitJob:
     """A set of fits with every input already resident on its device.
 
@@ -459,7 +462,6 @@ class FitJob:
         self.specs = specs
         self.epochs = epochs
         self.plan = plan_groups(specs, self.device)
-        split = split and split_allowed(len(self.plan))
         # (diagnostic: NERFHIP_PRIO_HEAVY=1 gives the heaviest group, the
         # sweep's critical path, a high-priority stream)
         heavy = os.environ.get("NERFHIP_PRIO_HEAVY", "0") == "1"
@@ -533,12 +535,8 @@ class FitJob:
 
     def outputs(self) -> list:
         outs = [None] * len(self.specs)
-        secs = self.group_seconds()
-        job_s = max(secs) if secs else 0.0          # the groups start together
-        job_f = sum(fit_flops(int(s.target.shape[0]), int(s.target.shape[1]), s.config,
-                              self.epochs) for s in self.specs)
-        for g, gs in zip(self.groups, secs):
-            for i, o in zip(g.members, g.outputs(self.specs, gs, job_s, job_f)):
+        for g, gs in zip(self.groups, self.group_seconds()):
+            for i, o in zip(g.members, g.outputs(self.specs, gs)):
                 outs[i] = o
         return outs
 
@@ -606,8 +604,8 @@ class StreamingJob:
     def _run(self, gi: int) -> None:
         try:
             d, members = self.plan[gi]
-            g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d,
-                       split_allowed(len(self.plan)), self.precision)
+            g = _Group(members, self.specs, self.epochs, self.lr, self.log_every, d, True,
+                       self.precision)
             self.groups[gi] = g
             g.ev_start.record(g.stream)
             desc = (_native.NerfhipGroup * 1)(g.desc)
@@ -658,17 +656,13 @@ class StreamingJob:
                 first = ev
         return max(first.elapsed_time(g.ev_end) for g in self.groups) / 1e3
 
-    def outputs(self, gi: int, job_seconds: float | None = None) -> list:
-        """[(fit index, FitOutput)] of finished group gi.  train_time_seconds:
-        with `job_seconds` (all groups done) the job's wall clock x the fit's
-        FLOP share, as FitJob.outputs; group_seconds is the group's own
-        measured device time either way."""
+    def outputs(self, gi: int) -> list:
+        """[(fit index, FitOutput)] of finished group gi; train_time_seconds
+        is the group's measured device time (FitOutput), known the moment the
+        group is done."""
         g = self.groups[gi]
         gs = g.ev_start.elapsed_time(g.ev_end) / 1e3
-        job_f = sum(fit_flops(int(p.target.shape[0]), int(p.target.shape[1]), p.config,
-                              self.epochs) for p in self.protos)
-        outs = g.outputs(self.specs, gs, job_seconds, job_f if job_seconds else None)
-        return list(zip(g.members, outs))
+        return list(zip(g.members, g.outputs(self.specs, gs)))
 
 
 def run_fits(specs: list, epochs: int, lr: float = 1e-4, log_every: int = 0,

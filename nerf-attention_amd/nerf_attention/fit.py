@@ -10,14 +10,18 @@ another (fit.py:54-76).  Here every model is first initialised on the host in
 the reference's loop order — init is the only consumer of the torch RNG, so
 each fit gets exactly the parameters the sequential reference would give it —
 and then ALL fits are trained together on the HIP engine (grouped by width,
-one stream per group, optionally over several GPUs).  The per-fit progress
-lines are printed afterwards, in the reference order.
+one stream per group, optionally over several GPUs).  Each fit's stdout block
+(the `[k/N] name` line, its probe lines and the `-> CosSim` line,
+fit.py:66-86) is printed as soon as its group has finished and every fit
+before it in the reference's record order has been printed, so stdout keeps
+the reference's order; a line per finished group goes to stderr.
 
 `train_time_seconds` (siren.py:96,117: the wall clock of the fit's epoch
-loop; summed over the reference's sequential sweep, its training time): the
-fits here train concurrently, so each gets the job's wall clock times its
-share of the job's FLOPs — a lone fit its own loop time, and the sum over a
-sweep the sweep's training wall clock (per GPU), as in the reference.
+loop) is measured: the device-clock interval of the group that trained the
+fit, from before its first launch to after its last (engine.FitOutput).  A
+lone fit gets its own loop time; fits of concurrent groups overlap, so a
+sweep's records sum to more than its wall clock (printed at the end by the
+CLI).
 
 With `gpus=N` (or `--gpus N`) the fits are farmed over N GPUs, one worker
 process per GPU (farm.run_farm), the same one-process-per-GPU design as
@@ -29,6 +33,7 @@ from __future__ import annotations
 import argparse
 import os
 import json
+import sys
 import time
 from pathlib import Path
 
@@ -82,18 +87,20 @@ def sweep_plan(layers, heads, configs, load_layer):
     return plan, skipped
 
 
-def _host_plan(plan, epochs: int, log_every: int):
+def _host_plan(plan, epochs: int, log_every: int, on_ready=None):
     """device='cpu' (BASELINE config 1): the fits one after the other in eager
     PyTorch, each model initialised right before its fit as the reference
-    does (fit.py:70-76)."""
+    does (fit.py:70-76); on_ready(k, result, probes) after each."""
     from .host_fit import fit_on_host
     out = []
-    for _name, _l, _h, _kv, cfg, tensor in plan:
+    for k, (_name, _l, _h, _kv, cfg, tensor) in enumerate(plan):
         m = SIREN(cfg, out_features=int(tensor.shape[1]))
         probes = []
         res = fit_on_host(tensor, cfg, m, epochs, 1e-4, log_every,
                           lambda *probe: probes.append(probe))
         out.append((res, probes))
+        if on_ready:
+            on_ready(k, res, probes)
     return out
 
 
@@ -126,16 +133,16 @@ def _stream_ok(plan, epochs, devices, log_every, precision) -> bool:
     return need <= engine.memory_budget(devices[0])
 
 
-def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precision=None):
+def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precision=None,
+                         on_ready=None):
     """train_plan with the host work overlapped (engine.StreamingJob): the
     inits are drawn in plan order (the reference's RNG order; siren.init_flat,
-    bit-identical to building each SIREN) and each group of consecutive same-width fits starts training the moment its last
-    init exists; finished groups are copied back and turned into FitResults
-    while the others still train.  (Checkpoints and stdout wait for the end:
-    each record, which both carry, holds train_time_seconds.)
-    train_time_seconds is the same attribution as train_plan's (the job's
-    wall clock x the fit's FLOP share), fixed up once every group is done;
-    each output's measured `group_seconds` is its group's own device time."""
+    bit-identical to building each SIREN) and each group of same-width fits
+    starts training the moment its last init exists; every finished group is
+    copied back and turned into FitResults while the others still train, and
+    on_ready(k, result, probes) is called for each of its fits (fit_kv_cache
+    prints and saves from there).  train_time_seconds: the group's measured
+    device time (engine.FitOutput)."""
     protos = [engine.FitSpec(target=tensor, config=cfg, init=None)
               for _n, _l, _h, _kv, cfg, tensor in plan]
     job = engine.StreamingJob(protos, epochs, log_every=log_every, device=device,
@@ -143,27 +150,29 @@ def train_plan_streaming(plan, epochs: int, device: int, log_every: int, precisi
     for k, (_name, _l, _h, _kv, cfg, tensor) in enumerate(plan):
         job.add(k, engine.FitSpec(target=tensor, config=cfg,
                                   init=init_flat(cfg, int(tensor.shape[1]))))
-    results, outs = [None] * len(plan), [None] * len(plan)
+    results = [None] * len(plan)
     dev = torch.device('cuda', device)
-    for gi in job.finished():
-        for k, o in job.outputs(gi):
+    for n, gi in enumerate(job.finished(), 1):
+        done = job.outputs(gi)
+        for k, o in done:
             n_rows, d = int(plan[k][5].shape[0]), int(plan[k][5].shape[1])
             m = uninitialised(plan[k][4], d, dev)
             m.load_flat_parameters(o.params)
             m.eval()
-            outs[k] = o
             results[k] = (_finish(m, plan[k][4], o, n_rows, d), o.probes)
-    job_s = job.job_seconds()
-    flops = [engine.fit_flops(int(p.target.shape[0]), int(p.target.shape[1]), p.config, epochs)
-             for p in protos]
-    tot = sum(flops) or 1.0
-    for k, (res, _p) in enumerate(results):
-        res.train_time_seconds = job_s * flops[k] / tot
-        outs[k].train_time_seconds = res.train_time_seconds
+        if done:
+            o = done[0][1]
+            print(f"[nerf-attention-amd] group {n}/{len(job.plan)} done: {len(done)} x "
+                  f"{plan[done[0][0]][4].name if len({plan[k][4].name for k, _ in done}) == 1 else 'mixed'}"
+                  f" (W={plan[done[0][0]][4].hidden_features}) in {o.group_seconds:.2f}s device time",
+                  file=sys.stderr, flush=True)
+        if on_ready:
+            for k, _o in done:
+                on_ready(k, *results[k])
     return results
 
 
-def train_plan(plan, epochs: int, devices, log_every: int, precision=None):
+def train_plan(plan, epochs: int, devices, log_every: int, precision=None, on_ready=None):
     """Draw every model's init in plan order (the reference's RNG order;
     siren.init_flat), then train them all on the engine; the returned models
     are built storage-only (siren.uninitialised) around the trained parameters.  Returns [(FitResult, probes)]."""
@@ -178,7 +187,62 @@ def train_plan(plan, epochs: int, devices, log_every: int, precision=None):
         m.eval()
         results.append((_finish(m, cfg, o, int(tensor.shape[0]), int(tensor.shape[1])),
                         o.probes))
+    if on_ready:
+        for k, (res, probes) in enumerate(results):
+            on_ready(k, res, probes)
     return results
+
+
+class _Report:
+    """The per-fit output of fit_kv_cache (fit.py:54-86) in the reference's
+    order — layer by layer, a missing layer's 'Skipping' line in its place,
+    then the layer's fits in plan order — each block (`[k/N] name`, the probe
+    lines, `-> CosSim`), record and medium checkpoint emitted the moment its
+    fit has finished and everything before it has been emitted."""
+
+    def __init__(self, plan, layers, skipped, total, epochs, output_dir):
+        self.plan, self.total, self.epochs, self.output_dir = plan, total, epochs, output_dir
+        self.order = []
+        for layer in layers:
+            if layer in skipped:
+                self.order.append(('skip', layer))
+            else:
+                self.order += [('fit', k) for k, p in enumerate(plan) if p[1] == layer]
+        self.ready, self.at, self.count, self.records = {}, 0, 0, []
+        self._flush()
+
+    def fit_done(self, k, res, probes):
+        self.ready[k] = (res, probes)
+        self._flush()
+
+    def _flush(self):
+        while self.at < len(self.order):
+            kind, v = self.order[self.at]
+            if kind == 'skip':
+                print(f"  Skipping layer {v} (not found)")
+            else:
+                if v not in self.ready:
+                    return
+                res, probes = self.ready.pop(v)
+                name, layer, head, kv_type, cfg, _t = self.plan[v]
+                self.count += 1
+                print(f"\n[{self.count}/{self.total}] {name}")
+                for ep, nm, rm, cs in probes:
+                    print(probe_line(ep, self.epochs, nm, rm, cs))
+                record = _result_to_record(name, layer, head, kv_type, res)
+                self.records.append(record)
+                if cfg.name == 'medium':
+                    _save_model(self.output_dir, name, res, record)
+                print(f"  -> CosSim: {res.final_cosine_mean:.4f} | "
+                      f"Compress: {res.compression_ratio:.1f}x | "
+                      f"Time: {res.train_time_seconds:.1f}s", flush=True)
+            self.at += 1
+
+    def finish(self) -> list:
+        self._flush()
+        if self.at != len(self.order):
+            raise RuntimeError(f"fit {self.order[self.at][1]} never reported")
+        return self.records
 
 
 def fit_kv_cache(
@@ -220,33 +284,16 @@ def fit_kv_cache(
 
     plan, skipped = sweep_plan(layers, heads, configs, load_layer)
     log_every = max(epochs // 5, 100)
+    report = _Report(plan, layers, skipped, total, epochs, output_dir)
     if host:
-        results = _host_plan(plan, epochs, log_every)
+        _host_plan(plan, epochs, log_every, on_ready=report.fit_done)
     elif _stream_ok(plan, epochs, devices, log_every, precision):
-        results = train_plan_streaming(plan, epochs, devices[0], log_every, precision)
+        train_plan_streaming(plan, epochs, devices[0], log_every, precision,
+                             on_ready=report.fit_done)
     else:
-        results = train_plan(plan, epochs, devices, log_every=log_every, precision=precision)
-
-    all_results: list[dict] = []
-    count = 0
-    for layer in layers:
-        if layer in skipped:
-            print(f"  Skipping layer {layer} (not found)")
-            continue
-        for (name, l, head, kv_type, cfg, _t), (res, probes) in zip(plan, results):
-            if l != layer:
-                continue
-            count += 1
-            print(f"\n[{count}/{total}] {name}")
-            for ep, nm, rm, cs in probes:
-                print(probe_line(ep, epochs, nm, rm, cs))
-            record = _result_to_record(name, layer, head, kv_type, res)
-            all_results.append(record)
-            if cfg.name == 'medium':
-                _save_model(output_dir, name, res, record)
-            print(f"  -> CosSim: {res.final_cosine_mean:.4f} | "
-                  f"Compress: {res.compression_ratio:.1f}x | "
-                  f"Time: {res.train_time_seconds:.1f}s")
+        train_plan(plan, epochs, devices, log_every=log_every, precision=precision,
+                   on_ready=report.fit_done)
+    all_results = report.finish()
 
     with open(output_dir / 'fit_results.json', 'w') as f:
         json.dump(all_results, f, indent=2)

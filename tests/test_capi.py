@@ -108,12 +108,13 @@ def test_group_plan(lib, monkeypatch):
     """nerfhip_group_plan (host only): BASELINE config 2, one medium fit at
     seq 2048 in bf16x3 with the split-K workspace, takes the K-split row kernel
     (one 16-row block per workgroup) and 8 gradient row slices on 64 x 64
-    tiles, reduced by the k_adam_split pass (three launches per epoch;
-    NERFHIP_SPLIT_FUSED=1 lets the last-arriving slice of each tile reduce it
-    inside the parameter kernel: two); a wide fit at 8192 (128 regular workgroups) K-split rows too and
-    128 x 128 tiles x 8 slices; a 40-fit W = 256
-    sweep chunk the 32-row kernel (128-row workgroups), fused; a 40-fit
-    W = 512 chunk the regular kernels."""
+    tiles, reduced by the k_adam_split pass (three launches per epoch); a
+    wide fit at 8192 (128 regular workgroups) K-split rows too and 128 x 128
+    tiles x 8 slices; 40-fit W = 256 and W = 512 sweep chunks the regular
+    kernels.  The opt-in switches of the variant kernels (NERFHIP_SPLIT_FUSED,
+    NERFHIP_ROWS32) change nothing in the product library, which does not
+    contain those kernels (nerfhip_build_flags bit NERFHIP_BUILD_VARIANTS)."""
+    assert lib.nerfhip_build_flags() & 8 == 0
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=1,
                   grad_partial=1)
     assert rc == 0
@@ -122,7 +123,7 @@ def test_group_plan(lib, monkeypatch):
     assert p.launches_per_epoch == 3
     monkeypatch.setenv("NERFHIP_SPLIT_FUSED", "1")
     assert _plan(lib, W=256, D=128, N=2048, n_fits=1, L_max=2, epochs=2000, precision=1,
-                 grad_partial=1)[1].launches_per_epoch == 2
+                 grad_partial=1)[1].launches_per_epoch == 3
     monkeypatch.delenv("NERFHIP_SPLIT_FUSED")
     rc, p = _plan(lib, W=512, D=128, N=8192, n_fits=1, L_max=3, epochs=2000, precision=1,
                   grad_partial=1)
@@ -130,12 +131,11 @@ def test_group_plan(lib, monkeypatch):
     assert p.params_workgroups == 8 * (3 * 16 + 1 * 4 + 512 // 64)     # 60 128x128 tiles
     monkeypatch.setenv("NERFHIP_ROWS32", "1")
     rc, p = _plan(lib, W=256, D=128, N=2048, n_fits=40, L_max=3, epochs=2000, precision=1)
-    assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (2, 1, 2)
-    assert p.rows_workgroups == 8 * 16 * 5                            # XCD map: 40 fits x 16
+    assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (0, 1, 2)
+    assert p.rows_workgroups == 8 * 32 * 5                            # XCD map: 40 fits x 32
     rc, p = _plan(lib, W=512, D=128, N=2048, n_fits=40, L_max=2, epochs=2000, precision=1)
     assert rc == 0 and (p.rows_variant, p.grad_split, p.launches_per_epoch) == (0, 1, 2)
     assert p.rows_workgroups == 8 * 32 * 5                            # XCD map: 40 fits x 32
-    # 32-row kernel only where 128-row workgroups tile the rows (n_pad % 128)
     rc, p = _plan(lib, W=256, D=128, N=1984, n_fits=40, L_max=2, epochs=2000, precision=1)
     assert rc == 0 and p.rows_variant == 0                            # n_pad 1984 = 15.5 x 128
     rc, p = _plan(lib, W=256, D=64, N=2048, n_fits=40, L_max=2, epochs=2000, precision=1)

@@ -69,9 +69,12 @@ def test_sweep_280_vs_reference(gpu, golden_dir, sweep):
 @pytest.mark.parametrize("world,rank", [(8, 0), (2, 1)])
 def test_rank_share_vs_reference(gpu, golden_dir, sweep, world, rank):
     """What one rank of a `world`-GPU farm trains, alone on one GPU: its
-    groups are smaller (at 8 ranks the W = 512, 128 and 64 groups hold 5 fits
-    each; they train concurrently, so none takes the split-K path:
-    engine.split_allowed), yet every fit stays within 1e-3."""
+    groups are smaller, yet every fit stays within 1e-3.  At 8 ranks the
+    W = 512, 128 and 64 groups hold 5 fits each, and the W = 128 and 64 ones
+    take the split-K weight-gradient path (16 row slices + k_adam_split)
+    WHILE the W = 256 and 512 groups train beside them on the same GPU — the
+    job of the round-5 concurrent split-K fault, whose containment
+    (engine.split_allowed) round 6 removed."""
     plan, specs = sweep
     ref = _ref_sweep(golden_dir)
     costs = [engine.fit_flops(2048, 128, s.config, 2000) for s in specs]
@@ -80,9 +83,11 @@ def test_rank_share_vs_reference(gpu, golden_dir, sweep, world, rank):
     d = np.array([abs(_cos(o) - ref[plan[i][0]]["final_cosine_mean"]) for i, o in zip(mine, outs)])
     assert d.max() <= COS_TOL, (d.max(), plan[mine[int(d.argmax())]][0])
     if world == 8:
-        job = engine.FitJob([specs[i] for i in mine], 1, devices=[0])
-        # several groups on one GPU: no split-K path (engine.split_allowed)
-        assert all(g.grad_partial is None for g in job.groups)
+        split = {(o.plan["grad_split"], o.plan["launches_per_epoch"]) for i, o in zip(mine, outs)
+                 if specs[i].config.hidden_features <= 128}
+        assert split == {(16, 3)}, split
+        assert {o.plan["grad_split"] for i, o in zip(mine, outs)
+                if specs[i].config.hidden_features >= 256} == {1}
 
 
 @pytest.mark.parametrize("seq_len", [512, 1024, 4096])
@@ -231,9 +236,9 @@ def test_fit_cli_quick(gpu, golden_dir, tmp_path):
 def test_farm_two_workers_equal_one_process(gpu, monkeypatch):
     """run_fits over two devices = two farm worker processes (here both on
     GPU 0): every fit bitwise equal to training it in this process.  (The
-    split-K path is off on both sides: whether it runs depends on how many
-    groups share a device, engine.split_allowed, which differs between a
-    worker's share and a lone fit.)"""
+    split-K path is off on both sides here: a worker's groups hold two tiny
+    fits, a lone fit is a one-fit group, and the split-K slice count follows
+    the group's grid; test_farm_lone_split_fits_bitwise covers split-K.)"""
     from nerf_attention.synthetic import kv_slice
     monkeypatch.setenv("NERFHIP_SPLIT_MAX_FITS", "0")
     keys, vals = kv_slice(5, 1, seq_len=256)
@@ -249,6 +254,32 @@ def test_farm_two_workers_equal_one_process(gpu, monkeypatch):
         alone = engine.run_fits([s], 40, devices=[0])[0]
         assert torch.equal(alone.params.cpu(), f.params.cpu())
         assert alone.losses == f.losses
+
+
+def test_farm_lone_split_fits_bitwise(gpu, monkeypatch):
+    """Split-K in and out of the farm: two fits of different
+    widths over two farm workers — each worker trains ONE one-fit group on the
+    split-K path — are bitwise the fits trained alone in this process, and
+    bitwise the same two fits trained together in one process (two concurrent
+    split-K groups on one device: the split choice depends on the group's
+    shape only, engine.wants_split)."""
+    from nerf_attention.synthetic import kv_slice
+    monkeypatch.delenv("NERFHIP_SPLIT_MAX_FITS", raising=False)
+    keys, vals = kv_slice(3, 2, seq_len=512)
+    cfgs = [SIRENConfig(256, 2, 30.0, "medium"), SIRENConfig(128, 1, 30.0, "small")]
+    specs = []
+    for i, c in enumerate(cfgs):
+        torch.manual_seed(10 + i)
+        specs.append(engine.FitSpec(target=(keys, vals)[i], config=c,
+                                    init=SIREN(c, 128).flat_parameters()))
+    farmed = engine.run_fits(specs, 60, devices=[0, 0])
+    together = engine.run_fits(specs, 60, devices=[0])
+    for s, f, t in zip(specs, farmed, together):
+        alone = engine.run_fits([s], 60, devices=[0])[0]
+        assert alone.plan["grad_split"] > 1 and t.plan["grad_split"] == alone.plan["grad_split"]
+        for o in (f, t):
+            assert torch.equal(alone.params.cpu(), o.params.cpu())
+            assert alone.losses == o.losses
 
 
 def test_forward_positions_autograd_and_short_inputs(gpu):

@@ -369,7 +369,7 @@ def _fake_streaming(monkeypatch, rc=0):
             self.desc = engine._native.NerfhipGroup()
             self.ev_start, self.ev_end = _FakeEvent(clock), _FakeEvent(clock)
 
-        def outputs(self, specs, gs, job_s, job_f):
+        def outputs(self, specs, gs):
             return [gs] * len(self.members)
 
     class FakeLib:
@@ -468,15 +468,21 @@ def test_init_replay_self_check(monkeypatch):
     assert torch.equal(a, b)
 
 
-def test_split_allowed_only_for_one_group(monkeypatch):
-    """The split-K weight-gradient path is given only to jobs that train one
-    group on the device (engine.split_allowed; DESIGN.md §12: an open fault
-    with concurrent split groups); NERFHIP_SPLIT_CONCURRENT=1 overrides."""
-    monkeypatch.delenv("NERFHIP_SPLIT_CONCURRENT", raising=False)
-    assert engine.split_allowed(1) and engine.split_allowed(0)
-    assert not engine.split_allowed(2) and not engine.split_allowed(4)
-    monkeypatch.setenv("NERFHIP_SPLIT_CONCURRENT", "1")
-    assert engine.split_allowed(4)
+def test_split_choice_depends_on_the_group_shape_only(monkeypatch):
+    """The split-K workspace goes to every group under 8 fits whose fused
+    parameter grid is under 128 workgroups, whatever else trains on the device
+    (round 5's engine.split_allowed, which withheld it from concurrent groups,
+    is gone: DESIGN.md §13).  The 8-rank share's 5-fit W = 128 / 64 groups take
+    it, its 5-fit W = 512 group (220 tiles) and 20-fit W = 256 group do not."""
+    monkeypatch.delenv("NERFHIP_SPLIT_MAX_FITS", raising=False)
+    assert not hasattr(engine, "split_allowed")
+    assert engine.wants_split(5, 128, 128, 1, 16) and engine.wants_split(5, 64, 128, 1, 16)
+    assert engine.wants_split(1, 256, 128, 2, 16) and engine.wants_split(1, 512, 128, 3, 16)
+    assert not engine.wants_split(5, 512, 128, 2, 16)      # 5 x 44 tiles >= 128
+    assert not engine.wants_split(20, 256, 128, 3, 16) and not engine.wants_split(8, 64, 128, 1, 16)
+    assert not engine.wants_split(1, 256, 128, 2, 1)       # no row slices to split into
+    monkeypatch.setenv("NERFHIP_SPLIT_MAX_FITS", "0")
+    assert not engine.wants_split(1, 256, 128, 2, 16)
 
 
 def test_ks_lds_hb_checker_on_synthetic_traces():

@@ -45,17 +45,26 @@ def test_every_step_kernel_present(ks):
               "k_transpose_params", "k_normalize", "k_row_metrics"):
         assert k in names, k
     # the fused parameter step in the K-split weight layout (KSX = kLayKs = 1)
-    # exists for every K-split width, and in the 32-row layout (kLay32 = 2) at W = 256
+    # exists for every K-split width
     for w in (128, 256, 512):
         assert f"void k_step_params<{w}, 128, true, false, 1, false>(nerfhip_detail::KArgs)" in ks
-    assert "void k_step_params<256, 128, true, false, 2, false>(nerfhip_detail::KArgs)" in ks
-    # unsplit and split-K (SK) instantiations of the regular tiles, small tiles split-K only
+    # regular tiles (unsplit, and split-K with the k_adam_split pass), and the
+    # 64 x 64 split-K tiles of lone W >= 256 fits
     for w in (64, 128, 256, 512):
-        for sk in ("false", "true"):
-            assert f"void k_step_params<{w}, 128, true, false, 0, {sk}>(nerfhip_detail::KArgs)" in ks
-    assert "void k_step_params<256, 128, true, true, 0, true>(nerfhip_detail::KArgs)" in ks
-    for t in ("true", "false"):
-        assert f"void k_step_rows32<256, 128, {t}>(nerfhip_detail::KArgs)" in ks
+        assert f"void k_step_params<{w}, 128, true, false, 0, false>(nerfhip_detail::KArgs)" in ks
+    assert "void k_step_params<256, 128, true, true, 0, false>(nerfhip_detail::KArgs)" in ks
+
+
+def test_product_library_has_no_opt_in_kernels(ks):
+    """the shipped library instantiates only kernels the
+    engine launches by default.  The 32-row row kernel and the fused split-K
+    reduction (measured slower) exist only in NERFHIP_VARIANTS
+    builds (tools/build_variant.py): no k_step_rows32, no SK = true parameter
+    kernel, no parameter kernel in the 32-row weight layout (KSX = 2)."""
+    names = list(ks)
+    assert not [n for n in names if "k_step_rows32" in n]
+    assert not [n for n in names if n.startswith("void k_step_params<") and n.endswith(", true>(nerfhip_detail::KArgs)")]
+    assert not [n for n in names if n.startswith("void k_step_params<") and ", 2, false>" in n]
 
 
 # the split-K parameter kernels (SK = true, groups under 8 fits): the fused

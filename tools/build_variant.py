@@ -4,6 +4,11 @@ from the main build (nerf_attention/_lib/obj), linked to
 build/variants/v_<name>.so.  Diagnostic only (kbench / ab.sh via NERFHIP_LIB).
 
 usage: python tools/build_variant.py <name> [-DFLAG ...] [--parts 6,8]
+
+The opt-in kernels that are not in the product library (the 32-row row
+kernel, the fused split-K reduction) need -DNERFHIP_VARIANTS over every part
+that launches them: the host part and the parameter parts, e.g.
+  python tools/build_variant.py variants -DNERFHIP_VARIANTS --parts 0,1,2,3,4,5,6,7,8
 """
 
 import subprocess
@@ -29,11 +34,10 @@ def main():
     base = [_build.HIPCC, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-fPIC",
             "-Wno-unused-function", "-I", str(_build.INCLUDE), *rest]
     objs, procs = [], []
-    units = ([(0, 0, [])] + [(p, k, _build.KIND_FLAGS[k]) for p in range(1, _build.N_PARTS)
-                             for k in _build.KIND_FLAGS] + _build.R32_UNITS)
+    units = _build.units(rest)
     for part, kind, flags in units:
         fname = f"nerfhip_p{part}.o" if kind == 0 else f"nerfhip_p{part}k{kind}.o"
-        if part in parts:
+        if part in parts or kind == 3:                  # (the 32-row unit: variant builds only)
             obj = odir / fname
             procs.append(subprocess.Popen(base + flags + [
                 f"-DNERFHIP_PART={part}", f"-DNERFHIP_KIND={kind}", "-c",
