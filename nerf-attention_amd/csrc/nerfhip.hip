@@ -39,6 +39,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
+#include <atomic>
 #include <stdlib.h>
 #include <math.h>
 #include <type_traits>
@@ -109,14 +111,110 @@ struct KArgs {
   // occupancy knob (a padded row workgroup cannot share its CU with a second
   // row workgroup, only with a parameter one); 0 = none (make_args)
   uint32_t rows_dyn_lds, params_dyn_lds;
+  // diagnostic builds only (NERFHIP_DIAG_FLIGHT): the launch's sequence number,
+  // its group, a hash of the arguments the host sent, and the host-mapped
+  // flight-recorder ring every workgroup marks on entry and exit
+  uint32_t seq, group;
+  uint64_t hash;
+  unsigned char* flight;
 };
 template <int W, int D, bool X3> int launch_rows(const KArgs& a, hipStream_t st);
 template <int W, int D, bool X3> int launch_params(const KArgs& a, hipStream_t st);
 template <int W, int D> int launch_rows32(const KArgs& a, hipStream_t st);
+
+// ---------------------------------------------------------------------------
+// Flight recorder (NERFHIP_DIAG_FLIGHT builds only; tools/r6/flight.py).
+// Every launch takes a slot of a host-mapped ring: the host writes what it
+// launched (sequence number, kernel, epoch, group, grid, argument hash); every
+// workgroup's thread 0 marks one byte on entry and one on exit, and checks the
+// arguments it received against the hash and the fit's depth against L_max
+// (a failed check is recorded and the workgroup returns without touching
+// memory).  After a device fault the ring names the launches in flight.
+// ---------------------------------------------------------------------------
+constexpr int kFlightRing = 4096, kFlightHdr = 128, kFlightMaxB = 2048;
+constexpr size_t kFlightSlot = kFlightHdr + 2 * (size_t)kFlightMaxB;
+__host__ __device__ inline uint64_t flight_mix(uint64_t h, uint64_t v) {
+  h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+  return h;
+}
+__host__ __device__ inline uint64_t kargs_hash(const KArgs& a) {
+  uint64_t h = 0x243f6a8885a308d3ull;
+  const uint64_t v[] = {
+      (uint64_t)a.W, (uint64_t)a.D, (uint64_t)a.N, (uint64_t)a.n_pad, (uint64_t)a.n_fits,
+      (uint64_t)a.L_max, (uint64_t)a.epochs, (uint64_t)a.epoch, (uint64_t)a.mode,
+      (uint64_t)a.p_stride, (uint64_t)a.pt_stride, (uint64_t)a.s_stride, (uint64_t)a.t_stride,
+      (uint64_t)a.lp_stride, (uint64_t)a.y_stride, (uint64_t)(uintptr_t)a.fit_layers,
+      (uint64_t)(uintptr_t)a.fit_omega, (uint64_t)(uintptr_t)a.pos, (uint64_t)(uintptr_t)a.target,
+      (uint64_t)(uintptr_t)a.tnorm, (uint64_t)(uintptr_t)a.params, (uint64_t)(uintptr_t)a.params_t,
+      (uint64_t)(uintptr_t)a.m, (uint64_t)(uintptr_t)a.v, (uint64_t)(uintptr_t)a.scratch,
+      (uint64_t)(uintptr_t)a.sched, (uint64_t)(uintptr_t)a.loss_partial, (uint64_t)(uintptr_t)a.y_out,
+      (uint64_t)a.n_split, (uint64_t)a.gp_stride, (uint64_t)(uintptr_t)a.gpart, (uint64_t)a.x3,
+      (uint64_t)a.ws_stride, (uint64_t)(uintptr_t)a.wsplit, (uint64_t)a.rows_ks,
+      (uint64_t)a.small_tiles, (uint64_t)a.seq, (uint64_t)a.group};
+  for (uint64_t x : v) h = flight_mix(h, x);
+  return h;
+}
+#ifdef NERFHIP_DIAG_FLIGHT
+KArgs flight_stamp(const KArgs& a, int kid, unsigned grid);   // host: assign seq, hash, header
+#define NERFHIP_KA(a, kid, grid) nerfhip_detail::flight_stamp((a), (kid), (unsigned)(grid))
+#else
+#define NERFHIP_KA(a, kid, grid) (a)
+#endif
 }  // namespace nerfhip_detail
 
 namespace {
 using nerfhip_detail::KArgs;
+
+#ifdef NERFHIP_DIAG_FLIGHT
+struct Flight {
+  unsigned char* s = nullptr;
+  unsigned b = 0;
+  __device__ explicit Flight(const KArgs& a) {
+    if (!a.flight) return;
+    s = a.flight + (size_t)(a.seq % nerfhip_detail::kFlightRing) * nerfhip_detail::kFlightSlot;
+    b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    if (threadIdx.x == 0 && b < nerfhip_detail::kFlightMaxB)
+      __hip_atomic_store(s + nerfhip_detail::kFlightHdr + b, (unsigned char)1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __device__ ~Flight() {
+    if (s && threadIdx.x == 0 && b < nerfhip_detail::kFlightMaxB)
+      __hip_atomic_store(s + nerfhip_detail::kFlightHdr + nerfhip_detail::kFlightMaxB + b,
+                         (unsigned char)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // header words 8.. (device side): 8 seq seen by workgroup 0, 9 its argument
+  // hash, 10 workgroups whose arguments failed the hash (flag), 11 depth out
+  // of range (flag)
+  __device__ void flag(int word, uint64_t v) {
+    if (s && threadIdx.x == 0)
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(s) + word, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __device__ bool args_ok(const KArgs& a) {
+    if (!s) return true;
+    KArgs c = a;
+    c.hash = 0;
+    const uint64_t h = nerfhip_detail::kargs_hash(c);
+    if (b == 0) { flag(8, a.seq); flag(9, h); }
+    if (h != a.hash) { flag(10, 1ull + b); return false; }
+    return true;
+  }
+  __device__ bool depth_ok(const KArgs& a, int L, int fit) {
+    if (!s) return true;
+    if (L >= 1 && L <= a.L_max && fit >= 0 && fit < a.n_fits) return true;
+    flag(11, ((uint64_t)(uint32_t)L << 32) | (uint32_t)fit);
+    return false;
+  }
+};
+#define FLIGHT_ENTER()            \
+  Flight flight_(a);              \
+  if (!flight_.args_ok(a)) return;
+#define FLIGHT_DEPTH(L, fit) \
+  if (!flight_.depth_ok(a, (L), (fit))) return;
+#else
+#define FLIGHT_ENTER()
+#define FLIGHT_DEPTH(L, fit)
+#endif
 
 
 
@@ -866,6 +964,7 @@ template <int W> struct RowsCfg {
 template <int W, int D, bool X3, bool TRAIN>
 __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIMD)
     k_step_rows(KArgs a) {
+  FLIGHT_ENTER();
   constexpr int NWV = RowsCfg<W>::NWAVES, NTH = RowsCfg<W>::THREADS;
   constexpr int JW = W / 16, JD = D / 16, KMAX = (W > D ? W : D);
   constexpr int NS = RowsCfg<W>::NSPLIT, JP = JW / NS;     // J tiles per pass
@@ -885,6 +984,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   const int c = lane & 15, g = lane >> 4;
   float* stash = lds + WBUF + 2 * KMAX + wave * STASH + lane * 4;
   const int L = fit_layers_of(a, fit);
+  FLIGHT_DEPTH(L, fit);
   const float om = a.fit_omega[fit];
   const int n_pad = a.n_pad;
   const int rblk = tile * NWV + wave;         // 16-row block
@@ -1396,6 +1496,7 @@ __device__ __forceinline__ void gemm_ks(const uint16_t* __restrict__ xs, int src
 
 template <int W, int D, int MODE>
 __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
+  FLIGHT_ENTER();
   static_assert(W >= 128 && D == 128, "K-split rows: W >= 128, D = 128");
   constexpr int JW = W / 16, JD = D / 16, PD = KsCfg<W>::PD;
   constexpr int NO = W / 64;                 // owned tiles of a W-wide output
@@ -1420,6 +1521,7 @@ __global__ void __launch_bounds__(256, 1) k_step_rows_ks(KArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, g = lane >> 4;
   const int L = fit_layers_of(a, fit);
+  FLIGHT_DEPTH(L, fit);
   const float om = a.fit_omega[fit];
   const int r = rblk * 16 + c;
   const bool valid = r < a.N;
@@ -2791,6 +2893,7 @@ template <int W, int D, bool X3, bool SMALL = false, int KSX = kLayX, bool SK = 
 __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
                                   (ParamsCfg<W, D, X3, SMALL>::MINB))
     k_step_params(KArgs a) {
+  FLIGHT_ENTER();
   using C = ParamsCfg<W, D, X3, SMALL>;
   constexpr int LDS_F = X3 ? 2 * 3 * (C::T + C::TK) * kFx / 2 : 2 * (2 * C::T) * kFs;
   __shared__ __attribute__((aligned(16))) float lds[LDS_F];
@@ -2801,6 +2904,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
   const int split = t / nt;
   t -= split * nt;
   const int L = fit_layers_of(a, fit);
+  FLIGHT_DEPTH(L, fit);
   if (t >= C::tiles(L)) return;
   const int nb = a.n_pad / 16 / a.n_split, rb0 = split * nb;
   // (the unsplit kernel keeps the run-time test: with G a compile-time null
@@ -2893,12 +2997,50 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
 // copy.  One thread per canonical parameter index; grid (ceil(P/256), n_fits).
 // (W, D compile-time: the index splits and split-copy addresses fold to
 // shifts and multiplies)
+//
+// Straight-line, with EXEC never narrowed: every lane loads from a valid
+// (clamped) index, and every store is a buffer store whose offset is pushed
+// past the resource's range for lanes that must not store (the hardware drops
+// it).  The round-5 version returned early for the lanes past the fit's last
+// parameter and branched per lane between the final-layer, hidden-layer and
+// bias cases, so EXEC was rewritten right after its stores; with this grid
+// running beside other groups' kernels, a store that waited behind the busy
+// memory pipeline wrote through lanes whose address registers were never set
+// (the concurrent split-K fault).  The wave also drains its
+// stores before it ends.
+constexpr uint32_t kOob = 0x80000000u;   // a byte offset past every resource below
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_over(const void* p, int64_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)nbytes, 0x00020000);
+}
+// an offset computed by every lane, then replaced by kOob where `keep` is
+// false: the volatile empty asm pins the computation ahead of the select (left
+// free, the compiler sank it into a branch per store, EXEC-masked)
+__device__ __forceinline__ uint32_t lane_off(bool keep, uint32_t off) {
+  asm volatile("" : "+v"(off));
+  return keep ? off : kOob;
+}
+// buffer resources held in their SGPRs up to this point (after a vmcnt(0)
+// drain: no store can still be waiting to read them)
+__device__ __forceinline__ void keep_live(__amdgpu_buffer_rsrc_t a, __amdgpu_buffer_rsrc_t b,
+                                          __amdgpu_buffer_rsrc_t c) {
+  asm volatile("" ::"s"(a), "s"(b), "s"(c));
+}
+__device__ __forceinline__ void bstore_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void bstore_u16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, (int)off, 0, 0);
+}
 template <int W, int D, int NS>
 __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
+  FLIGHT_ENTER();
   const int fit = blockIdx.y;
   const int L = fit_layers_of(a, fit);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n_params(W, D, L)) return;
+  FLIGHT_DEPTH(L, fit);
+  const int64_t n = n_params(W, D, L);
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool ok = i0 < n;
+  const int64_t i = ok ? i0 : 0;                  // a valid index for every lane's loads
   const float* g = a.gpart + fit * a.gp_stride + i;
   // every slice's load in flight at once (NS = n_split, compile-time): a
   // runtime-count loop compiled to load → vmcnt(0) → add per slice, 15 serial
@@ -2909,32 +3051,72 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   float gs = gv[0];
 #pragma unroll
   for (int sp = 1; sp < NS; ++sp) gs += gv[sp];   // slice order
-  float* P = a.params + fit * a.p_stride;
-  float* M = a.m + fit * a.p_stride;
-  float* V = a.v + fit * a.p_stride;
+  const float* P = a.params + fit * a.p_stride;
+  const float* M = a.m + fit * a.p_stride;
+  const float* V = a.v + fit * a.p_stride;
   float p = P[i], mm = M[i], vv = V[i];
   adam_update(p, mm, vv, gs, a.sched[2 * a.epoch], a.sched[2 * a.epoch + 1]);
-  P[i] = p; M[i] = mm; V[i] = vv;
-  float* PT = a.params_t + fit * a.pt_stride;
-  uint16_t* XS = a.x3 ? a.wsplit + fit * a.ws_stride : nullptr;
+  const int64_t pbytes = 4 * a.p_stride;
+  const uint32_t po = lane_off(ok, (uint32_t)(4 * i));
+  const __amdgpu_buffer_rsrc_t pr = rsrc_over(P, pbytes), mr = rsrc_over(M, pbytes),
+                               vr = rsrc_over(V, pbytes);
+  bstore_f32(pr, po, p);
+  bstore_f32(mr, po, mm);
+  bstore_f32(vr, po, vv);
 #ifdef NERFHIP_EXP_ADAM_NO_SPLIT_COPIES   // diagnostic (wrong results): cost of the split-copy stores
-  if (XS) return;
-#endif
-  const int64_t fw = off_final_w(W, L);
-  if (i >= fw) {                                       // Wf [D][W] → Wfᵀ [W][D]
-    const int64_t r = i - fw;
-    if (r < (int64_t)D * W) {
-      if (XS) put_w(XS, wlayout(a), W, D, L, L + 1, (int)(r / W), (int)(r % W), p);
-      else PT[(int64_t)L * W * W + (r % W) * D + r / W] = p;
-    }
-  } else if (i >= 2 * W) {                             // Wi [W][W] → Wiᵀ
-    const int64_t r = (i - 2 * W) % ((int64_t)W * W + W);
-    const int64_t layer = (i - 2 * W) / ((int64_t)W * W + W);
-    if (r < (int64_t)W * W) {
-      if (XS) put_w(XS, wlayout(a), W, D, L, (int)layer + 1, (int)(r / W), (int)(r % W), p);
-      else PT[layer * W * W + (r % W) * W + r / W] = p;
-    }
+  if (a.x3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    keep_live(pr, mr, vr);
+    return;
   }
+#endif
+  // which weight (if any) parameter i is: matrix mi (1..L hidden, L+1 final),
+  // element [j][k]; `wt` false for biases and the first layer.  32-bit
+  // arithmetic with compile-time divisors (a 64-bit division would branch
+  // per lane on the operands' high words)
+  const int ii = (int)i, fw = (int)off_final_w(W, L);
+  const bool fin = ii >= fw;
+  const int ih = ii - 2 * W < 0 ? 0 : ii - 2 * W;
+  const int rh = ih % (W * W + W);
+  const int r = fin ? ii - fw : rh;
+  // (bitwise, not short-circuit: && here compiled to EXEC-masked branches)
+  const bool wt = ok & ((fin & (r < D * W)) | (!fin & (ii >= 2 * W) & (rh < W * W)));
+  const int mi = fin ? L + 1 : ih / (W * W + W) + 1;
+  const int j = wt ? r / W : 0, k = wt ? r % W : 0;
+  if (a.x3) {                                     // (kernel arguments: scalar branches)
+    const uint16_t* XS = a.wsplit + fit * a.ws_stride;
+    const __amdgpu_buffer_rsrc_t xr = rsrc_over(XS, 2 * a.ws_stride);
+    const int R = mi <= L ? W : D;
+    const int f = (int)xs_mat(W, D, L, false, mi), bk = (int)xs_mat(W, D, L, true, mi);
+    uint32_t h, m, l;
+    split3(p, h, m, l);
+    const uint16_t part[3] = {(uint16_t)(h >> 16), (uint16_t)(m >> 16), (uint16_t)(l >> 16)};
+    auto copies = [&](auto lay_c) {
+      constexpr int lay = decltype(lay_c)::value;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        bstore_u16(xr, lane_off(wt, (uint32_t)(2 * (f + (int)xoff_any(lay, R, W, j, k, pl)))), part[pl]);
+        bstore_u16(xr, lane_off(wt, (uint32_t)(2 * (bk + (int)xoff_any(lay, W, R, k, j, pl)))), part[pl]);
+      }
+    };
+    if (a.rows_ks) copies(std::integral_constant<int, kLayKs>{});
+    else copies(std::integral_constant<int, kLayX>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    keep_live(xr, xr, xr);
+  } else {
+    // both candidates computed by every lane, then selected (a `fin ? a : b`
+    // of the two expressions compiled to an EXEC-masked branch)
+    uint32_t tf = (uint32_t)(4 * (L * W * W + k * D + j)), th = (uint32_t)(4 * ((mi - 1) * W * W + k * W + j));
+    asm volatile("" : "+v"(tf), "+v"(th));
+    const __amdgpu_buffer_rsrc_t tr = rsrc_over(a.params_t + fit * a.pt_stride, 4 * a.pt_stride);
+    bstore_f32(tr, lane_off(wt, fin ? tf : th), p);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    keep_live(tr, tr, tr);
+  }
+  // every store drained before the wave ends, and its resource registers kept
+  // until then (the compiler otherwise reuses them right after the last store)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  keep_live(pr, mr, vr);
 }
 
 // ---------------------------------------------------------------------------
@@ -2948,6 +3130,7 @@ __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
 // order through LDS (deterministic), then every thread normalises its rows.
 constexpr int kNormCols = 64, kNormRowGroups = 16;
 __global__ void __launch_bounds__(kNormCols * kNormRowGroups) k_normalize(KArgs a) {
+  FLIGHT_ENTER();
   __shared__ double part[kNormRowGroups][kNormCols];
   const int fit = blockIdx.y;
   const int c = threadIdx.x & (kNormCols - 1), rg = threadIdx.x / kNormCols;
@@ -2989,9 +3172,11 @@ __global__ void __launch_bounds__(kNormCols * kNormRowGroups) k_normalize(KArgs 
 // params_t ← transposed copies of every hidden weight and of the final weight
 // (fp32 precision); wsplit ← both split copies (bf16x3 precision).
 __global__ void k_transpose_params(KArgs a) {
+  FLIGHT_ENTER();
   const int fit = blockIdx.y;
   // the same depth the step kernels train (a one-fit group: L_max, nerfhip.h)
   const int L = fit_layers_of(a, fit);
+  FLIGHT_DEPTH(L, fit);
   const int W = a.W, D = a.D;
   const int64_t nh = (int64_t)L * W * W, total = nh + (int64_t)W * D;
   const float* P = a.params + fit * a.p_stride;
@@ -3020,6 +3205,7 @@ __global__ void k_transpose_params(KArgs a) {
 // (siren.py:109-111, 122-125).  One wave per row.
 __global__ void k_row_metrics(KArgs a, const float* ybuf, int64_t ystride,
                               float* row_cos, float* row_sq, int64_t rstride) {
+  FLIGHT_ENTER();
   const int fit = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
@@ -3126,6 +3312,10 @@ KArgs make_args(const nerfhip_group* g, const nerfhip_sizes& s) {
   if (const char* e = getenv("NERFHIP_ROWS_LDS_PAD")) a.rows_dyn_lds = pad_kb(e);
   if (const char* e = getenv("NERFHIP_PARAMS_LDS_PAD")) a.params_dyn_lds = pad_kb(e);
 #endif
+#ifdef NERFHIP_DIAG_FLIGHT
+  if (const char* e = getenv("NERFHIP_FLIGHT"))
+    a.flight = reinterpret_cast<unsigned char*>(strtoull(e, nullptr, 0));
+#endif
 #if defined(NERFHIP_STAMPS) || defined(NERFHIP_EXP_KS_TRACE)
   if (const char* e = getenv("NERFHIP_PSTAMPS"))
     a.pstamps = reinterpret_cast<unsigned long long*>(strtoull(e, nullptr, 0));
@@ -3172,11 +3362,12 @@ int launch_rows(const KArgs& a, hipStream_t st) {
 #endif
 #ifdef NERFHIP_EXP_KS_MODES
       if (a.mode == 0)
-        hipLaunchKernelGGL((k_step_rows_ks<W, D, 0>), dim3(grid), dim3(256), dyn, st, a);
+        hipLaunchKernelGGL((k_step_rows_ks<W, D, 0>), dim3(grid), dim3(256), dyn, st, NERFHIP_KA(a, 200000 + W * 100 + D, grid));
       else
-        hipLaunchKernelGGL((k_step_rows_ks<W, D, 1>), dim3(grid), dim3(256), dyn, st, a);
+        hipLaunchKernelGGL((k_step_rows_ks<W, D, 1>), dim3(grid), dim3(256), dyn, st, NERFHIP_KA(a, 200000 + W * 100 + D, grid));
 #else
-      hipLaunchKernelGGL((k_step_rows_ks<W, D, -1>), dim3(grid), dim3(256), dyn, st, a);
+      hipLaunchKernelGGL((k_step_rows_ks<W, D, -1>), dim3(grid), dim3(256), dyn, st,
+                         NERFHIP_KA(a, 200000 + W * 100 + D, grid));
 #endif
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
@@ -3189,10 +3380,10 @@ int launch_rows(const KArgs& a, hipStream_t st) {
   const int grid = grid_for(a.n_fits, a.n_pad / RowsCfg<W>::ROWS);
   if (a.mode == 0)
     hipLaunchKernelGGL((k_step_rows<W, D, X3, true>), dim3(grid), dim3(RowsCfg<W>::THREADS),
-                       a.rows_dyn_lds, st, a);
+                       a.rows_dyn_lds, st, NERFHIP_KA(a, 100000 + W * 100 + D, grid));
   else
     hipLaunchKernelGGL((k_step_rows<W, D, X3, false>), dim3(grid), dim3(RowsCfg<W>::THREADS), 0,
-                       st, a);
+                       st, NERFHIP_KA(a, 100000 + W * 100 + D, grid));
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
@@ -3202,10 +3393,10 @@ template <int W, int D>
 int launch_adam_split(const KArgs& a, hipStream_t st) {
   const dim3 grid((unsigned)((n_params(W, D, a.L_max) + 255) / 256), a.n_fits);
   switch (a.n_split) {
-    case 2: hipLaunchKernelGGL((k_adam_split<W, D, 2>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((k_adam_split<W, D, 4>), grid, dim3(256), 0, st, a); break;
-    case 8: hipLaunchKernelGGL((k_adam_split<W, D, 8>), grid, dim3(256), 0, st, a); break;
-    case 16: hipLaunchKernelGGL((k_adam_split<W, D, 16>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((k_adam_split<W, D, 2>), grid, dim3(256), 0, st, NERFHIP_KA(a, 400000 + W * 100 + D, grid.x * grid.y)); break;
+    case 4: hipLaunchKernelGGL((k_adam_split<W, D, 4>), grid, dim3(256), 0, st, NERFHIP_KA(a, 400000 + W * 100 + D, grid.x * grid.y)); break;
+    case 8: hipLaunchKernelGGL((k_adam_split<W, D, 8>), grid, dim3(256), 0, st, NERFHIP_KA(a, 400000 + W * 100 + D, grid.x * grid.y)); break;
+    case 16: hipLaunchKernelGGL((k_adam_split<W, D, 16>), grid, dim3(256), 0, st, NERFHIP_KA(a, 400000 + W * 100 + D, grid.x * grid.y)); break;
     default: return NERFHIP_ERR_LAUNCH;
   }
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
@@ -3224,7 +3415,8 @@ int launch_params(const KArgs& a, hipStream_t st) {
         return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
       }
 #endif
-      hipLaunchKernelGGL((k_step_params<W, D, X3, true>), dim3(grid_s), dim3(CS::THREADS), 0, st, a);
+      hipLaunchKernelGGL((k_step_params<W, D, X3, true>), dim3(grid_s), dim3(CS::THREADS), 0, st,
+                         NERFHIP_KA(a, 300000 + W * 100 + D, grid_s));
       return launch_adam_split<W, D>(a, st);
     }
   }
@@ -3234,7 +3426,7 @@ int launch_params(const KArgs& a, hipStream_t st) {
   if constexpr (X3 && W >= 128 && D == 128) {
     if (a.rows_ks && a.n_split == 1) {   // fused epilogue writes the K-split layout
       hipLaunchKernelGGL((k_step_params<W, D, X3, false, kLayKs>), dim3(grid),
-                         dim3(ParamsCfg<W, D, X3>::THREADS), 0, st, a);
+                         dim3(ParamsCfg<W, D, X3>::THREADS), 0, st, NERFHIP_KA(a, 300000 + W * 100 + D, grid));
       return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
     }
   }
@@ -3253,7 +3445,7 @@ int launch_params(const KArgs& a, hipStream_t st) {
   }
 #endif
   hipLaunchKernelGGL((k_step_params<W, D, X3>), dim3(grid), dim3(ParamsCfg<W, D, X3>::THREADS),
-                     a.params_dyn_lds, st, a);
+                     a.params_dyn_lds, st, NERFHIP_KA(a, 300000 + W * 100 + D, grid));
   if (a.n_split > 1) return launch_adam_split<W, D>(a, st);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
@@ -3355,7 +3547,8 @@ void pick(int W, int D, bool x3, launch_fn* rows, launch_fn* params) {
 int row_metrics(const KArgs& a, const float* ybuf, int64_t ystride, float* rc, float* rs,
                 int64_t rstride, hipStream_t st) {
   dim3 grid((unsigned)((a.n_pad + 3) / 4), (unsigned)a.n_fits);
-  hipLaunchKernelGGL(k_row_metrics, grid, dim3(256), 0, st, a, ybuf, ystride, rc, rs, rstride);
+  hipLaunchKernelGGL(k_row_metrics, grid, dim3(256), 0, st, NERFHIP_KA(a, 700000, grid.x * grid.y), ybuf,
+                     ystride, rc, rs, rstride);
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
@@ -3385,7 +3578,7 @@ int nerfhip_build_flags(void) {
 #ifdef NERFHIP_STAMPS
   f |= NERFHIP_BUILD_STAMPS;
 #endif
-#if defined(NERFHIP_DIAG_ROWS_TWICE) || defined(NERFHIP_DIAG_ENV)
+#if defined(NERFHIP_DIAG_ROWS_TWICE) || defined(NERFHIP_DIAG_ENV) || defined(NERFHIP_DIAG_FLIGHT)
   f |= NERFHIP_BUILD_DIAG;
 #endif
 #ifdef NERFHIP_VARIANTS
@@ -3393,6 +3586,43 @@ int nerfhip_build_flags(void) {
 #endif
   return f;
 }
+
+#ifdef NERFHIP_DIAG_FLIGHT
+}  // extern "C"
+// host side of the flight recorder: a launch's sequence number, argument hash
+// and the slot header of what was launched (written before the launch)
+KArgs nerfhip_detail::flight_stamp(const KArgs& a, int kid, unsigned grid) {
+  static std::atomic<uint32_t> next{1};
+  KArgs b = a;
+  b.seq = next.fetch_add(1);
+  b.hash = 0;
+  b.hash = kargs_hash(b);
+  if (b.flight) {
+    unsigned char* s = b.flight + (size_t)(b.seq % kFlightRing) * kFlightSlot;
+    memset(s, 0, kFlightSlot);
+    volatile uint64_t* h = reinterpret_cast<volatile uint64_t*>(s);
+    h[1] = (uint64_t)kid;
+    h[2] = (uint64_t)(uint32_t)b.epoch | ((uint64_t)b.group << 32) | ((uint64_t)b.mode << 48);
+    h[3] = grid;
+    h[4] = b.hash;
+    h[5] = (uint64_t)b.n_split | ((uint64_t)b.n_fits << 16) | ((uint64_t)b.L_max << 32);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    h[0] = b.seq;   // last: a slot whose word 0 is set is complete
+  }
+  return b;
+}
+extern "C" {
+// diagnostic build only: the flight-recorder ring in host-mapped, coherent
+// memory (the device writes it with system-scope stores; readable after a
+// device fault)
+void* nerfhip_debug_flight_alloc(void) {
+  void* p = nullptr;
+  const size_t n = (size_t)nerfhip_detail::kFlightRing * nerfhip_detail::kFlightSlot;
+  if (hipHostMalloc(&p, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  memset(p, 0, n);
+  return p;
+}
+#endif
 
 #ifdef NERFHIP_STAMPS
 // diagnostic build only: device buffer of [blocks][4 waves][8] u64 stamps
@@ -3478,8 +3708,10 @@ int prologue(GroupRun& r) {
                          (size_t)(r.s.grad_partial - r.a.ctr_off) * sizeof(float), r.st) != hipSuccess)
         return NERFHIP_ERR_LAUNCH;
   hipLaunchKernelGGL(k_normalize, dim3((g->D + kNormCols - 1) / kNormCols, g->n_fits),
-                     dim3(kNormCols * kNormRowGroups), 0, r.st, r.a);
-  hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st, r.a);
+                     dim3(kNormCols * kNormRowGroups), 0, r.st,
+                     NERFHIP_KA(r.a, 500000, ((g->D + kNormCols - 1) / kNormCols) * g->n_fits));
+  hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st,
+                     NERFHIP_KA(r.a, 600000, 64 * g->n_fits));
   return hipGetLastError() == hipSuccess ? NERFHIP_OK : NERFHIP_ERR_LAUNCH;
 }
 
@@ -3580,6 +3812,7 @@ static int fit_impl(const nerfhip_group* groups, int32_t n_groups, void* const* 
   int rc = NERFHIP_OK, max_epochs = 0;
   for (int i = 0; i < n_groups && rc == NERFHIP_OK; ++i) {
     runs[i] = make_run(&groups[i], streams[i]);
+    runs[i].a.group = (uint32_t)i;
     if (groups[i].epochs > max_epochs) max_epochs = groups[i].epochs;
     rc = select_device(groups[i].device, &cur);
     if (rc == NERFHIP_OK) rc = prologue(runs[i]);
@@ -3653,7 +3886,8 @@ int nerfhip_siren_forward(const nerfhip_group* g, void* stream) {
   r.a.y_out = g->eval_y;
   r.a.y_stride = r.s.target;
   if (r.a.x3) {   // the split weight copies of the current params
-    hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st, r.a);
+    hipLaunchKernelGGL(k_transpose_params, dim3(64, g->n_fits), dim3(256), 0, r.st,
+                       NERFHIP_KA(r.a, 600000, 64 * g->n_fits));
     if (hipGetLastError() != hipSuccess) return NERFHIP_ERR_LAUNCH;
   }
   rc = r.rows(r.a, r.st);

@@ -145,3 +145,15 @@ def test_spawn_ranks_propagates_failure(tmp_path):
     t0 = __import__("time").time()
     rc = farm.spawn_ranks(2, [], str(script))
     assert rc == 3 and __import__("time").time() - t0 < 20   # rank 0 was terminated
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_dry_run_leaves_no_child(gpus):
+    """bench.py reports the processes it started that are still alive when it
+    exits (the driver's record showed one process outliving the
+    bench); the dry run — rank spawn, gloo group, shares, barrier, gather — ends
+    with none."""
+    r = _sp.run([_sys.executable, str(_BENCH), "--gpus", str(gpus), "--dry-run"],
+                env=_bench_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "children at exit: 0" in r.stderr, r.stderr[-2000:]

@@ -8,6 +8,7 @@ layout): parity tests cannot see that, so the resource metadata is pinned
 here.  The regular bf16x3 row kernel at W = 256 keeps its documented spills
 (two waves per SIMD beat one wave with no spills by 25 %)."""
 
+import re
 import shutil
 import sys
 from pathlib import Path
@@ -117,3 +118,56 @@ def test_ksplit_loads_have_no_late_operand_hazard():
                    if "k_step_rows_ks" in k and (v[0] or v[1])}
             assert not bad, bad
     assert seen, "no K-split kernel found in the library"
+
+
+def _functions(dis: str):
+    """{mangled name: [instruction text]} of an llvm-objdump -d listing."""
+    out, name = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(_Z\w+)>:$", line)
+        if m:
+            name = m.group(1)
+            out[name] = []
+            continue
+        s = re.sub(r"\s*//.*", "", line).strip()
+        if name and s:
+            out[name].append(s)
+    return out
+
+
+def test_adam_split_stores_are_never_exec_masked():
+    """The concurrent split-K fault of rounds 5-6 was
+    k_adam_split's: lanes past the fit's last parameter returned early and the
+    final-layer / hidden-layer / bias cases branched per lane, so its stores ran
+    under narrowed EXEC, restored one to three instructions after the store;
+    with the grid beside other groups' kernels the device faulted on an address
+    whose low word was a valid split-weight address of the group and whose high
+    word was not.  The kernel is now straight-line: for every instantiation in
+    the shipped library, no instruction writes EXEC, every store is a buffer
+    store (lanes masked by an out-of-range offset), and every wave drains its
+    stores (s_waitcnt vmcnt(0)) before s_endpgm."""
+    import subprocess
+    import tempfile
+    if not (kernel_resources.LLVM / "llvm-objdump").exists():
+        pytest.skip("llvm-objdump missing")
+    seen = 0
+    with tempfile.TemporaryDirectory() as t:
+        for co in kernel_resources.code_objects(kernel_resources.LIB, Path(t)):
+            dis = subprocess.run([str(kernel_resources.LLVM / "llvm-objdump"), "-d",
+                                  "--mcpu=gfx950", str(co)], capture_output=True, text=True,
+                                 check=True).stdout
+            for name, body in _functions(dis).items():
+                if "k_adam_split" not in name:
+                    continue
+                seen += 1
+                exec_w = [s for s in body if s.startswith("s_") and "exec" in s
+                          and not s.startswith(("s_cbranch_execz", "s_cbranch_execnz"))]
+                assert not exec_w, (name, exec_w[:3])
+                stores = [s for s in body if "store" in s.split()[0]]
+                assert stores and all(s.startswith("buffer_store") for s in stores), (name, stores[:3])
+                for k, s in enumerate(body):
+                    if s.startswith("s_endpgm"):
+                        prev = [p for p in body[:k] if not p.startswith(("s_mov", "s_nop"))]
+                        assert prev and prev[-1].startswith("s_waitcnt") and "vmcnt(0)" in prev[-1], \
+                            (name, body[max(0, k - 4):k + 1])
+    assert seen >= 64, seen          # 4 widths x 2 head dims x 4 slice counts, per part
