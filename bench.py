@@ -241,8 +241,8 @@ ISO_EPOCHS = 101   # isolated leg: 25 timed launches (every 4th epoch from epoch
 # the committed rocprofv3 summary of exactly that leg (tools/r4/iso_prof.sh runs
 # tools/r4/isokernel.py, which calls isolated_kernel below, under
 # rocprofv3 --kernel-trace --stats, and its PMC passes)
-ISO_PROFILE = "profiles/r05/rocprof_kernel_stats_isolated_rows256.csv"
-ISO_PMC = ROOT / "profiles" / "r05" / "pmc_isolated_rows256.json"
+ISO_PROFILE = "profiles/r06/rocprof_kernel_stats_isolated_256.csv"
+ISO_PMC = ROOT / "profiles" / "r06" / "pmc_isolated_256.json"
 
 
 def lib_sha16() -> str:
@@ -486,10 +486,18 @@ def main() -> None:
             iso = isolated_kernel([my_specs[i] for i in gsel], kname, g_flops,
                                   args.precision, peak, local)
             iso["fits"] = len(gsel)
-            iso_pmc = committed_pmc(ISO_PMC, f"{kname}[{args.precision}]", lib_sha16())
+            sha = lib_sha16()
+            iso_pmc = committed_pmc(ISO_PMC, f"{kname}[{args.precision}]", sha)
             iso_bytes = iso_pmc and iso_pmc.get("bytes")
             hbm_iso = iso_bytes and iso_bytes / (iso["avg_launch_ms"] * 1e-3) / 1e9
             alg_bytes = sum(4 * N * 128 + 24 * c.num_parameters(128) for c in gcf)
+            # the chunk-epoch: the row and the parameter kernel of the same
+            # isolated group, both counted
+            pname = (kname.replace("k_step_rows", "k_step_params") if "rows" in kname
+                     else kname.replace("k_step_params", "k_step_rows"))
+            partner_pmc = committed_pmc(ISO_PMC, f"{pname}[{args.precision}]", sha)
+            partner_bytes = partner_pmc and partner_pmc.get("bytes")
+            epoch_bytes = iso_bytes and partner_bytes and iso_bytes + partner_bytes
             roof = {"bound": "mfma", "achieved": iso["achieved"],
                     "peak": round(peak, 1), "unit": "TFLOP/s",
                     "frac": iso["frac"],
@@ -506,13 +514,18 @@ def main() -> None:
                     "traffic_detail": iso_pmc,
                     "traffic_source": "rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of the "
                                       "same isolated group (tools/r4/iso_prof.sh, "
-                                      "profiles/r05/pmc_isolated_rows256.json)",
+                                      f"{ISO_PMC.relative_to(ROOT)})",
                     "mfma_busy": iso_pmc and iso_pmc.get("mfma_busy"),
                     "algorithmic_bytes": alg_bytes,
                     "algorithmic_bytes_kind": "SURVEY.md §8d per fit-epoch 4·N·D target + 24·P "
                                               "params/Adam read+write, x fits of the group "
                                               "(activations assumed on-chip)",
-                    "traffic_over_algorithmic": iso_bytes and round(iso_bytes / alg_bytes, 2),
+                    "traffic_chunk_epoch": epoch_bytes,
+                    "traffic_chunk_epoch_kind": f"PMC bytes of {kname} + {pname} per epoch of "
+                                                "the isolated group (FETCH_SIZE x2 + WRITE_SIZE)",
+                    "partner_traffic_detail": partner_pmc,
+                    "traffic_over_algorithmic": epoch_bytes and round(epoch_bytes / alg_bytes, 2),
+                    "dominant_over_algorithmic": iso_bytes and round(iso_bytes / alg_bytes, 2),
                     "mfma_busy_kind": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GPU-active "
                                       "cycles), rocprofv3 PMC pass of the same isolated group",
                     "hbm_gbs": hbm_iso and round(hbm_iso, 1),

@@ -30,19 +30,15 @@ def lib_sha16() -> str:
     return hashlib.sha256(Path(lib).read_bytes()).hexdigest()[:16]
 
 
-def main():
-    d = Path(sys.argv[1])
-    ev = None
-    for line in (d / "trace.log").read_text().splitlines():
-        if line.startswith("{"):
-            ev = json.loads(line)
+def summarise(d: Path, ev: dict, kind: str, hip_ms: float) -> tuple:
+    """Per-launch PMC figures and the rocprof average of one kernel kind
+    (`k_step_rows` / `k_step_params`) of the isolated leg."""
     W = int(ev["kernel"].split("<")[1].split(",")[0])
-    kind = ev["kernel"].split("<")[0]
     x3 = "true" if ev["precision"] == "bf16x3" else "false"
     pat = re.compile(rf"{kind}<{W}, 128, {x3}, (true|false)(, false)*>" if kind == "k_step_rows"
                      else rf"{kind}<{W}, 128, {x3}, false(, false)?(, \d+)?(, false)?>")
-    # the 32-row training kernel (k_step_rows32<W, 128, TRAIN>) stands in for
-    # k_step_rows when the library selects it
+    # the 32-row training kernel (k_step_rows32<W, 128, TRAIN>, variant builds)
+    # stands in for k_step_rows when the library selects it
     pat32 = re.compile(rf"k_step_rows32<{W}, 128, true>")
 
     def match(name):
@@ -68,7 +64,7 @@ def main():
     rd = 2 * 1024 * per.get("FETCH_SIZE", 0.0)
     wr = 1024 * per.get("WRITE_SIZE", 0.0)
     key = f"{kind}<{W},128>[{ev['precision']}]"
-    out = {key: {
+    return key, {
         "bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
         "mfma_busy": (per["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * per["GRBM_GUI_ACTIVE"] / N_XCD)
                       if per.get("GRBM_GUI_ACTIVE") else None),
@@ -76,11 +72,30 @@ def main():
         "rocprof_avg_ms": stats and round(stats["avg_ms"], 5),
         "rocprof_calls": stats and stats["calls"],
         "rocprof_min_ms": stats and round(stats["min_ms"], 5),
-        "hipevent_avg_ms": ev["avg_launch_ms"],
-        "rocprof_vs_hipevent": stats and round(stats["avg_ms"] / ev["avg_launch_ms"] - 1, 4),
-        "flops_per_launch": ev["flops_per_launch"], "fits": ev["fits"], "epochs": ev["epochs"],
+        "hipevent_avg_ms": hip_ms,
+        "rocprof_vs_hipevent": stats and round(stats["avg_ms"] / hip_ms - 1, 4),
+        "fits": ev["fits"], "epochs": ev["epochs"],
         "lib_sha16": lib_sha16(),
-        "source": "tools/r4/iso_prof.sh (rocprofv3 of tools/r4/isokernel.py)"}}
+        "source": "tools/r4/iso_prof.sh (rocprofv3 of tools/r4/isokernel.py)"}
+
+
+def main():
+    """Both kernels of the isolated chunk-epoch (the leg launches the row and
+    the parameter kernel once per epoch; bench.py reports their bytes together
+    against SURVEY.md §8d's algorithmic bytes of the chunk-epoch)."""
+    d = Path(sys.argv[1])
+    ev = None
+    for line in (d / "trace.log").read_text().splitlines():
+        if line.startswith("{"):
+            ev = json.loads(line)
+    primary = ev["kernel"].split("<")[0]
+    partner = "k_step_params" if primary == "k_step_rows" else "k_step_rows"
+    out = {}
+    for kind, ms in ((primary, ev["avg_launch_ms"]), (partner, ev["partner_kernel_avg_ms"])):
+        key, rec = summarise(d, ev, kind, ms)
+        if kind == primary:
+            rec["flops_per_launch"] = ev["flops_per_launch"]
+        out[key] = rec
     print(json.dumps(out, indent=1))
 
 
