@@ -257,6 +257,16 @@ __device__ unsigned long long* g_stamps = nullptr;
       a.pstamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =             \
           __builtin_amdgcn_s_memrealtime();                                            \
   } while (0)
+// slots 5, 6 of the parameter kernel's wave record: HW_ID (CU / SIMD / SE)
+// and XCC_ID, read once at entry
+#define PSTAMP_HW()                                                                    \
+  do {                                                                                 \
+    if (a.pstamps && (threadIdx.x & 63) == 0) {                                        \
+      const size_t o_ = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8;            \
+      a.pstamps[o_ + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);                   \
+      a.pstamps[o_ + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 20);                  \
+    }                                                                                  \
+  } while (0)
 // the K-split row kernel's stamps, after the parameter kernel's 4096 x 4 x 8
 #define KSTAMP(k)                                                                      \
   do {                                                                                 \
@@ -273,6 +283,9 @@ __device__ unsigned long long* g_stamps = nullptr;
   } while (0)
 #define PSTAMP(k) \
   do {            \
+  } while (0)
+#define PSTAMP_HW() \
+  do {              \
   } while (0)
 #define KSTAMP(k) \
   do {            \
@@ -540,6 +553,35 @@ __device__ __forceinline__ int fit_layers_of(const KArgs& a, int fit) {
 // the weight-plane layout the group's row kernel reads
 __host__ __device__ inline int wlayout(const KArgs& a) {
   return a.rows_ks ? kLayKs : a.rows32 ? kLay32 : kLayX;
+}
+
+// Buffer-resource helpers (k_adam_split's masked stores, the parameter
+// kernels' Adam epilogues).
+constexpr uint32_t kOob = 0x80000000u;   // a byte offset past every resource below
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_over(const void* p, int64_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)nbytes, 0x00020000);
+}
+// an offset computed by every lane, then replaced by kOob where `keep` is
+// false: the volatile empty asm pins the computation ahead of the select (left
+// free, the compiler sank it into a branch per store, EXEC-masked)
+__device__ __forceinline__ uint32_t lane_off(bool keep, uint32_t off) {
+  asm volatile("" : "+v"(off));
+  return keep ? off : kOob;
+}
+// buffer resources held in their SGPRs up to this point (after a vmcnt(0)
+// drain: no store can still be waiting to read them)
+__device__ __forceinline__ void keep_live(__amdgpu_buffer_rsrc_t a, __amdgpu_buffer_rsrc_t b,
+                                          __amdgpu_buffer_rsrc_t c) {
+  asm volatile("" ::"s"(a), "s"(b), "s"(c));
+}
+__device__ __forceinline__ void bstore_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void bstore_u16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ float bload_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
 
 // A split-K partial-slab element.  For the fused reduction (split_finish)
@@ -2657,27 +2699,70 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   PSTAMP(3);
 
   // Adam on the wave's (TJ/2)×(TK/WK) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
+  // The gradient is hi + lo.  The epilogue streams the (x, y) sub-tiles: the
+  // P/M/V loads of sub-tile s + 1 are issued before sub-tile s's Adam and
+  // stores, so a wave waits on one memory round trip per sub-tile instead of
+  // one per parameter (in-order vmcnt: a load issued after a store cannot be
+  // waited on without that store's acknowledgement too).  Buffer loads and
+  // stores over the layer's weights with one lane offset: no per-element
+  // 64-bit address arithmetic.  Arithmetic and its order are unchanged.
 #pragma unroll
   for (int x = 0; x < NA; ++x)
 #pragma unroll
-    for (int y = 0; y < NB; ++y) {
+    for (int y = 0; y < NB; ++y)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) hi[x][y][q] += lo[x][y][q];
+  if (G) {
+#pragma unroll
+    for (int x = 0; x < NA; ++x)
+#pragma unroll
+      for (int y = 0; y < NB; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int j = j0 + wj * (TJ / 2) + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int kcol = k0 + wk * (TK / WK) + 32 * y + lr;
+          slab_store<WT>(G + pw + (int64_t)j * W + kcol, hi[x][y][e]);
+        }
+  } else {
+    constexpr int NS = NA * NB;
+    constexpr int64_t kBytes = (int64_t)kOD * W * 4;
+    const __amdgpu_buffer_rsrc_t rp = rsrc_over(P + pw, kBytes), rm = rsrc_over(M + pw, kBytes),
+                                 rv = rsrc_over(V + pw, kBytes);
+    const uint32_t lb =
+        (uint32_t)(((j0 + wj * (TJ / 2) + 4 * h) * W + k0 + wk * (TK / WK) + lr) * 4);
+    auto eoff = [&](int sub, int e) {
+      return lb + (uint32_t)(((32 * (sub / NB) + 8 * (e >> 2) + (e & 3)) * W + 32 * (sub % NB)) * 4);
+    };
+    // half sub-tiles (8 parameters per lane) per round trip, double-buffered
+    float pq[2][8], mq[2][8], vq[2][8];
+    auto fetch = [&](int c, int buf) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t o = eoff(c >> 1, 8 * (c & 1) + e);
+        pq[buf][e] = bload_f32(rp, o);
+        mq[buf][e] = bload_f32(rm, o);
+        vq[buf][e] = bload_f32(rv, o);
+      }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int c = 0; c < 2 * NS; ++c) {
+      const int buf = c & 1, sub = c >> 1, x = sub / NB, y = sub % NB;
+      if (c + 1 < 2 * NS) fetch(c + 1, buf ^ 1);
       const int jrow0 = j0 + wj * (TJ / 2) + 32 * x;
       const int kcol = k0 + wk * (TK / WK) + 32 * y + lr;
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb) {
+      for (int qb = 2 * (c & 1); qb < 2 * (c & 1) + 2; ++qb) {
         uint32_t th[4], tm[4], tl[4];
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const int j = jrow0 + qq + 8 * qb + 4 * h;
-          const int64_t idx = pw + (int64_t)j * W + kcol;
-          const float gsum = hi[x][y][qb * 4 + qq] + lo[x][y][qb * 4 + qq];
-          if (G) {
-            slab_store<WT>(G + idx, gsum);
-            continue;
-          }
-          float p = P[idx], mm = M[idx], vv = V[idx];
-          adam_update(p, mm, vv, gsum, step_size, bc2s);
-          P[idx] = p; M[idx] = mm; V[idx] = vv;
+          const int e = qb * 4 + qq, j = jrow0 + qq + 8 * qb + 4 * h;
+          const uint32_t o = eoff(sub, e);
+          float p = pq[buf][e & 7], mm = mq[buf][e & 7], vv = vq[buf][e & 7];
+          adam_update(p, mm, vv, hi[x][y][e], step_size, bc2s);
+          bstore_f32(rp, o, p);
+          bstore_f32(rm, o, mm);
+          bstore_f32(rv, o, vv);
           split3(p, th[qq], tm[qq], tl[qq]);
 #ifndef NERFHIP_EXP_NO_FWDCOPY   // diagnostic build only: timing of the copy's stores
           // forward copy M[j][kcol] of [out_dim][W]
@@ -2686,17 +2771,17 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
           XS[xf + xoff_any(KSX, kOD, W, j, kcol, 2)] = (uint16_t)(tl[qq] >> 16);
 #endif
         }
-        if (!G) {   // transposed copy: Mᵀ[kcol][j..j+3] is one 8-B run per plane
-          const int jb = jrow0 + 8 * qb + 4 * h;
-          const u2 vh = {pk_top(th[0], th[1]), pk_top(th[2], th[3])};
-          const u2 vm = {pk_top(tm[0], tm[1]), pk_top(tm[2], tm[3])};
-          const u2 vl = {pk_top(tl[0], tl[1]), pk_top(tl[2], tl[3])};
-          *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 0)) = vh;
-          *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 1)) = vm;
-          *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 2)) = vl;
-        }
+        // transposed copy: Mᵀ[kcol][j..j+3] is one 8-B run per plane
+        const int jb = jrow0 + 8 * qb + 4 * h;
+        const u2 vh = {pk_top(th[0], th[1]), pk_top(th[2], th[3])};
+        const u2 vm = {pk_top(tm[0], tm[1]), pk_top(tm[2], tm[3])};
+        const u2 vl = {pk_top(tl[0], tl[1]), pk_top(tl[2], tl[3])};
+        *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 0)) = vh;
+        *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 1)) = vm;
+        *reinterpret_cast<u2*>(XS + xb + xoff_any(KSX, W, kOD, kcol, jb, 2)) = vl;
       }
     }
+  }
   if (do_bias_tile) {
 #pragma unroll
     for (int m = 0; m < NPA; ++m) {
@@ -2900,6 +2985,7 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
   int fit, t;
   const int nt = C::tiles(a.L_max);
   PSTAMP(0);
+  PSTAMP_HW();
   if (!map_block(blockIdx.x, a.n_fits, nt * a.n_split, fit, t)) return;
   const int split = t / nt;
   t -= split * nt;
@@ -3008,29 +3094,6 @@ __global__ void __launch_bounds__((ParamsCfg<W, D, X3, SMALL>::THREADS),
 // memory pipeline wrote through lanes whose address registers were never set
 // (the concurrent split-K fault).  The wave also drains its
 // stores before it ends.
-constexpr uint32_t kOob = 0x80000000u;   // a byte offset past every resource below
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_over(const void* p, int64_t nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)nbytes, 0x00020000);
-}
-// an offset computed by every lane, then replaced by kOob where `keep` is
-// false: the volatile empty asm pins the computation ahead of the select (left
-// free, the compiler sank it into a branch per store, EXEC-masked)
-__device__ __forceinline__ uint32_t lane_off(bool keep, uint32_t off) {
-  asm volatile("" : "+v"(off));
-  return keep ? off : kOob;
-}
-// buffer resources held in their SGPRs up to this point (after a vmcnt(0)
-// drain: no store can still be waiting to read them)
-__device__ __forceinline__ void keep_live(__amdgpu_buffer_rsrc_t a, __amdgpu_buffer_rsrc_t b,
-                                          __amdgpu_buffer_rsrc_t c) {
-  asm volatile("" ::"s"(a), "s"(b), "s"(c));
-}
-__device__ __forceinline__ void bstore_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 0);
-}
-__device__ __forceinline__ void bstore_u16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint16_t v) {
-  __builtin_amdgcn_raw_buffer_store_b16(v, r, (int)off, 0, 0);
-}
 template <int W, int D, int NS>
 __global__ void __launch_bounds__(256) k_adam_split(KArgs a) {
   FLIGHT_ENTER();
