@@ -2688,6 +2688,11 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
     // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
     gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
+    // the block loads stay at the top: left free, the scheduler sank them to
+    // just before the barrier, and the next block's split (interleaved with
+    // its MFMAs) then waited on them at once — a full load latency exposed
+    // per block instead of hidden behind one block of MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     mfma_block(rb);
     lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
     __syncthreads();
