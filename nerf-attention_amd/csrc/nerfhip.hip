@@ -2468,6 +2468,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
     // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
     gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
+    __builtin_amdgcn_sched_barrier(0);   // loads at the top (as in dw_tile_x3)
     const int off = (rb & 1) * BUF;
     f4 av[NA][2], bv[NB][2];
 #pragma unroll
@@ -2502,31 +2503,64 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
   }
 
   // Adam on the wave's (TJ/2)×(TK/WK) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
+  // Streamed as in dw_tile_x3: the P/M/V loads of the next half sub-tile are
+  // issued before the current one's Adam and stores.
+  if (G) {
 #pragma unroll
-  for (int x = 0; x < NA; ++x)
+    for (int x = 0; x < NA; ++x)
 #pragma unroll
-    for (int y = 0; y < NB; ++y) {
+      for (int y = 0; y < NB; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int j = j0 + wj * (TJ / 2) + 32 * x + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int kcol = k0 + wk * (TK / WK) + 32 * y + lr;
+          slab_store<WT>(G + pw + (int64_t)j * a.W + kcol, acc[x][y][e]);
+        }
+  } else {
+    constexpr int NS = NA * NB;
+    const int64_t nbytes = (int64_t)out_dim * a.W * 4;
+    const __amdgpu_buffer_rsrc_t rp = rsrc_over(P + pw, nbytes), rm = rsrc_over(M + pw, nbytes),
+                                 rv = rsrc_over(V + pw, nbytes);
+    const uint32_t lb =
+        (uint32_t)(((j0 + wj * (TJ / 2) + 4 * h) * a.W + k0 + wk * (TK / WK) + lr) * 4);
+    auto eoff = [&](int sub, int e) {
+      return lb + (uint32_t)(((32 * (sub / NB) + 8 * (e >> 2) + (e & 3)) * a.W + 32 * (sub % NB)) * 4);
+    };
+    float pq[2][8], mq[2][8], vq[2][8];
+    auto fetch = [&](int c, int buf) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t o = eoff(c >> 1, 8 * (c & 1) + e);
+        pq[buf][e] = bload_f32(rp, o);
+        mq[buf][e] = bload_f32(rm, o);
+        vq[buf][e] = bload_f32(rv, o);
+      }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int c = 0; c < 2 * NS; ++c) {
+      const int buf = c & 1, sub = c >> 1, x = sub / NB, y = sub % NB;
+      if (c + 1 < 2 * NS) fetch(c + 1, buf ^ 1);
       const int jrow0 = j0 + wj * (TJ / 2) + 32 * x;
       const int kcol = k0 + wk * (TK / WK) + 32 * y + lr;
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb) {
+      for (int qb = 2 * (c & 1); qb < 2 * (c & 1) + 2; ++qb) {
         f4 pt;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
-          const int j = jrow0 + qq + 8 * qb + 4 * h;
-          const int64_t idx = pw + (int64_t)j * a.W + kcol;
-          if (G) {
-            slab_store<WT>(G + idx, acc[x][y][qb * 4 + qq]);
-            continue;
-          }
-          float p = P[idx], mm = M[idx], vv = V[idx];
-          adam_update(p, mm, vv, acc[x][y][qb * 4 + qq], step_size, bc2s);
-          P[idx] = p; M[idx] = mm; V[idx] = vv;
+          const int e = qb * 4 + qq;
+          const uint32_t o = eoff(sub, e);
+          float p = pq[buf][e & 7], mm = mq[buf][e & 7], vv = vq[buf][e & 7];
+          adam_update(p, mm, vv, acc[x][y][e], step_size, bc2s);
+          bstore_f32(rp, o, p);
+          bstore_f32(rm, o, mm);
+          bstore_f32(rv, o, vv);
           pt[qq] = p;
         }
-        if (!G) st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
+        st4(PT + ptw + (int64_t)kcol * out_dim + jrow0 + 8 * qb + 4 * h, pt);
       }
     }
+  }
   if (do_bias) {
 #pragma unroll
     for (int x = 0; x < NA; ++x) {
@@ -2596,6 +2630,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
 
   static_assert(NA4 % 64 == 0, "A rows must fill whole waves (stage_slot permutes within 64)");
   auto gload = [&](f4 (&st)[NPT], int rb) {
+#ifdef NERFHIP_EXP_HOTBLOCK   // diagnostic timing build, WRONG numerics: every block re-reads block 0/1
+    rb &= 1;
+#endif
 #pragma unroll
     for (int m = 0; m < NPT; ++m) {
       const int i = tid + NTH * m;
@@ -3636,7 +3673,7 @@ int nerfhip_build_flags(void) {
     defined(NERFHIP_EXP_KS_ALTFIT) || defined(NERFHIP_EXP_KS_LINEAR) ||                      \
     defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
     defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
-    defined(NERFHIP_EXP_KS_TRACE) ||                                                          \
+    defined(NERFHIP_EXP_KS_TRACE) || defined(NERFHIP_EXP_HOTBLOCK) ||                        \
     defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
     defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
     defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \

@@ -1,7 +1,7 @@
 """Train a fixed set of groups (all widths, split-K and fused reductions,
 d_head 64 and 128) for a few epochs and save every fit's parameters and
 losses; run it under two NERFHIP_LIB builds and compare the files bitwise.
-usage: python tools/bitwise_ab.py out.npz   |   python tools/bitwise_ab.py --cmp a.npz b.npz"""
+usage: python tools/bitwise_ab.py out.npz [bf16x3|fp32]   |   python tools/bitwise_ab.py --cmp a.npz b.npz"""
 import sys
 from pathlib import Path
 
@@ -20,6 +20,7 @@ def main():
     import torch
     from nerf_attention import SIREN, SIRENConfig, engine
     from nerf_attention.synthetic import kv_slice
+    precision = sys.argv[2] if len(sys.argv) > 2 else "bf16x3"
     out = {}
     cases = [("medium40", SIRENConfig(256, 2, 30.0, "medium"), 40, 512, 128),
              ("deep9", SIRENConfig(256, 3, 30.0, "deep"), 9, 512, 128),
@@ -40,7 +41,7 @@ def main():
             torch.manual_seed(i)
             specs.append(engine.FitSpec(target=(k if i % 2 else v)[:, :D].contiguous(), config=cfg,
                                         init=SIREN(cfg, D).flat_parameters()))
-        outs = engine.run_fits(specs, 12, devices=[0], precision="bf16x3")
+        outs = engine.run_fits(specs, 12, devices=[0], precision=precision)
         for i, o in enumerate(outs):
             out[f"{name}_{i}_params"] = o.params.cpu().numpy()
             out[f"{name}_{i}_losses"] = np.asarray(o.losses, np.float32)
