@@ -1879,8 +1879,11 @@ __device__ __forceinline__ void r32_prefetch(const uint16_t* src, uint16_t* ring
 //               k-steps, a 16-B store's issue stall sits beside MFMAs
 //               instead of in a burst ahead of them (≈870 cycles per tile
 //               as a burst, profiles/r05/stamps32b_*.log).
-// NST / NLD: the exact store / load instruction counts of a whole flush(J) /
-// pre (or fewer: fewer only over-waits).
+// NST / NLD: the store / load instruction counts of a whole flush(J) / pre,
+// exact or fewer (fewer only over-waits).  The final layer passes the count
+// of a plain training flush (4); on a probe epoch (y_out set) its flush also
+// stores ŷ and issues 8, an undercount of the same safe kind, and so does
+// the next phase's NAFTER.
 // Phase boundaries.  The phase's first NR32 - 1 sub-chunks were issued before
 // it (r32_prefetch), followed by NAFTER vector-memory ops (the previous
 // phase's last two flushes, or layer 0's stores; fewer only over-waits), and
@@ -2956,7 +2959,11 @@ __device__ __forceinline__ void split_finish_run(const KArgs& a, int fit, int L,
 // drains them (vmcnt 0), then one lane draws a ticket from the tile's
 // monotonic counter (agent-scope relaxed add, no release fence needed), and
 // the reducer's lane acquires (this CU's L1 invalidated) before any wave
-// reads a slab.  The "I am last" word lives in the block's one LDS array (a second
+// reads a slab.  Under the HIP/C++ memory model a relaxed ticket after relaxed
+// stores is NOT a happens-before edge: correctness rests on gfx950's sc1
+// write-through stores having reached the agent-coherent L2 once vmcnt has
+// drained — an ISA-level argument, one reason this path stays an opt-in
+// variant (a default would take a release RMW on the ticket).  The "I am last" word lives in the block's one LDS array (a second
 // __shared__ object can de-pipeline the staging loop).
 template <class C, int W, int D, bool X3>
 __device__ void split_finish(const KArgs& a, int fit, int L, int t, float* lds) {
