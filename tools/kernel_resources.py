@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import re
 import struct
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -24,9 +25,13 @@ FIELDS = ("private_segment_fixed_size", "vgpr_count", "agpr_count", "sgpr_count"
 
 
 def code_objects(lib: Path, tmp: Path) -> list[Path]:
-    fb = tmp / "fatbin"
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", str(lib)], check=True,
-                   capture_output=True)
+    # objcopy rewrites its input file when given no output: dump from a copy,
+    # so the shipped library (and the hash the PMC summaries are stamped with)
+    # never changes under a resource check
+    fb, cp = tmp / "fatbin", tmp / "lib_copy.so"
+    shutil.copyfile(lib, cp)
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", str(cp), str(tmp / "lib_out.so")],
+                   check=True, capture_output=True)
     data = fb.read_bytes()
     out = []
     for s in (m.start() for m in re.finditer(re.escape(MAGIC), data)):
