@@ -513,3 +513,42 @@ def test_ks_lds_hb_checker_on_synthetic_traces():
     raw = trace({0: [(3, 1, 512)], 1: [(3, 0, 512)]})          # write -> read, same interval
     war = trace({0: [(5, 0, 768)], 2: [(5, 1, 768)]})          # read -> overwrite
     assert hb.check(raw)["races"] == 1 and hb.check(war)["races"] == 1
+
+
+def test_fit_report_streams_blocks_in_reference_order(capsys, tmp_path):
+    """fit_kv_cache's progress (reference fit.py:54-86):
+    each fit's block prints the moment it and every fit before it in the
+    reference's order have finished — layer by layer, a missing layer's
+    'Skipping' line in its place — whatever order the groups finish in, and the
+    records come out in that same order with the measured train time."""
+    from types import SimpleNamespace
+    from nerf_attention.fit import RECORD_KEYS, _Report
+    from nerf_attention.types import SIRENConfig
+
+    tiny, small = SIRENConfig(64, 1, 30.0, "tiny"), SIRENConfig(128, 1, 30.0, "small")
+    plan = [(f"L{l}_H0_key_{c.name}", l, 0, "key", c, None) for l in (0, 2) for c in (tiny, small)]
+
+    def res(k):
+        return SimpleNamespace(config=plan[k][4], final_mse=0.1, final_cosine_mean=0.9 + k / 100,
+                               final_cosine_min=0.8, final_cosine_std=0.01, compression_ratio=4.0,
+                               raw_size_bytes=1, siren_size_bytes=1, train_time_seconds=1.5 + k,
+                               num_parameters=10, seq_len=16, d_head=8)
+
+    rep = _Report(plan, layers=[0, 1, 2], skipped={1}, total=len(plan), epochs=10,
+                  output_dir=tmp_path)
+    assert capsys.readouterr().out == ""              # nothing before fit 0
+    rep.fit_done(2, res(2), [])                       # a later group finishes first
+    assert capsys.readouterr().out == ""              # still waiting for fits 0, 1
+    rep.fit_done(0, res(0), [(5, 0.5, 0.25, 0.75)])
+    out = capsys.readouterr().out
+    assert "[1/4] L0_H0_key_tiny" in out and "Epoch 5/10" in out and "[2/4]" not in out
+    rep.fit_done(1, res(1), [])
+    out = capsys.readouterr().out                     # fit 1, the skipped layer, then fit 2
+    assert out.index("[2/4] L0_H0_key_small") < out.index("Skipping layer 1") < \
+        out.index("[3/4] L2_H0_key_tiny")
+    rep.fit_done(3, res(3), [])
+    records = rep.finish()
+    assert [r["name"] for r in records] == [p[0] for p in plan]
+    assert [r["train_time_seconds"] for r in records] == [1.5, 2.5, 3.5, 4.5]
+    assert list(records[0]) == list(RECORD_KEYS)
+    assert "Time: 4.5s" in capsys.readouterr().out
