@@ -2734,6 +2734,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     // per block instead of hidden behind one block of MFMAs
     __builtin_amdgcn_sched_barrier(0);
     mfma_block(rb);
+#ifdef NERFHIP_EXP_SPLIT_AFTER_MFMA   // diagnostic: no interleaving of the split with the MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
     __syncthreads();
   };
@@ -3681,6 +3684,7 @@ int nerfhip_build_flags(void) {
     defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
     defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
     defined(NERFHIP_EXP_KS_TRACE) || defined(NERFHIP_EXP_HOTBLOCK) ||                        \
+    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) ||                                                 \
     defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
     defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
     defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \
