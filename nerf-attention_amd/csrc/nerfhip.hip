@@ -2738,6 +2738,16 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     __builtin_amdgcn_sched_barrier(0);
 #endif
     lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
+#ifdef NERFHIP_EXP_PARAMS_VPG   // experiment: an even VALU/MFMA interleave, VPG VALU per MFMA
+    // (the fragment reads first, then per MFMA: VPG VALU and every other MFMA one LDS store)
+    __builtin_amdgcn_sched_group_barrier(0x100, 6 * (NA + NB), 0);
+#pragma unroll
+    for (int i = 0; i < 6 * NA * NB; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, NERFHIP_EXP_PARAMS_VPG, 0);
+      if (i & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+    }
+#endif
     __syncthreads();
   };
   for (int rb = 0; rb < n_blocks; rb += 2) {
@@ -3684,7 +3694,7 @@ int nerfhip_build_flags(void) {
     defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
     defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
     defined(NERFHIP_EXP_KS_TRACE) || defined(NERFHIP_EXP_HOTBLOCK) ||                        \
-    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) ||                                                 \
+    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) || defined(NERFHIP_EXP_PARAMS_VPG) ||              \
     defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
     defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
     defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \
