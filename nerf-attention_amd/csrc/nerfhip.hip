@@ -2595,6 +2595,7 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // staging registers.  The Adam epilogue writes P/M/V and, instead of the
 // transposed fp32 copy, both split copies of the weights for the row kernel.
 constexpr int kFx = 24;
+constexpr int kParamsVpg = 6;   // VALU per MFMA in dw_tile_x3's block schedule
 
 template <int TJ, int TK, int NW, int WW, int OD, int KSX, bool WT = false>
 __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
@@ -2738,16 +2739,18 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     __builtin_amdgcn_sched_barrier(0);
 #endif
     lstore(st_fill, lds + ((rb + 1) & 1) * BUFX, rb + 1 < n_blocks);   // last: unread buffer
-#ifdef NERFHIP_EXP_PARAMS_VPG   // experiment: an even VALU/MFMA interleave, VPG VALU per MFMA
-    // (the fragment reads first, then per MFMA: VPG VALU and every other MFMA one LDS store)
-    __builtin_amdgcn_sched_group_barrier(0x100, 6 * (NA + NB), 0);
+    // An even interleave of the split with the MFMAs (sched_group_barrier):
+    // the fragment reads first, then per MFMA kParamsVpg VALU and every other
+    // MFMA one LDS store.  Deep × 40 isolated: 6 per MFMA 0.320 ms against
+    // 0.331 for the compiler's own order (3: 0.336, 4: 0.327, 8: 0.325,
+    // 12: 0.331; tools/sessions/r6/s6_27.sh, s6_28.sh).  Bitwise equal.
+    __builtin_amdgcn_sched_group_barrier(0x100, 3 * (NA + NB), 0);
 #pragma unroll
     for (int i = 0; i < 6 * NA * NB; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, NERFHIP_EXP_PARAMS_VPG, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, kParamsVpg, 0);
       if (i & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
     }
-#endif
     __syncthreads();
   };
   for (int rb = 0; rb < n_blocks; rb += 2) {
@@ -3694,7 +3697,7 @@ int nerfhip_build_flags(void) {
     defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
     defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
     defined(NERFHIP_EXP_KS_TRACE) || defined(NERFHIP_EXP_HOTBLOCK) ||                        \
-    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) || defined(NERFHIP_EXP_PARAMS_VPG) ||              \
+    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) ||                                                 \
     defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
     defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
     defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \
