@@ -2595,7 +2595,10 @@ __device__ __forceinline__ void dw_tile(const KArgs& a, const float* __restrict_
 // staging registers.  The Adam epilogue writes P/M/V and, instead of the
 // transposed fp32 copy, both split copies of the weights for the row kernel.
 constexpr int kFx = 24;
-constexpr int kParamsVpg = 6;   // VALU per MFMA in dw_tile_x3's block schedule
+#ifndef NERFHIP_PARAMS_VPG
+#define NERFHIP_PARAMS_VPG 6
+#endif
+constexpr int kParamsVpg = NERFHIP_PARAMS_VPG;   // VALU per MFMA in dw_tile_x3's block schedule
 
 template <int TJ, int TK, int NW, int WW, int OD, int KSX, bool WT = false>
 __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restrict__ A, int FA,
