@@ -2737,6 +2737,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
     // its MFMAs) then waited on them at once — a full load latency exposed
     // per block instead of hidden behind one block of MFMAs
     __builtin_amdgcn_sched_barrier(0);
+#ifdef NERFHIP_EXP_PARAMS_PRIO   // diagnostic: raised wave priority over the MFMA section
+    __builtin_amdgcn_s_setprio(NERFHIP_EXP_PARAMS_PRIO);
+#endif
     mfma_block(rb);
 #ifdef NERFHIP_EXP_SPLIT_AFTER_MFMA   // diagnostic: no interleaving of the split with the MFMAs
     __builtin_amdgcn_sched_barrier(0);
@@ -2754,6 +2757,9 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
       __builtin_amdgcn_sched_group_barrier(0x002, kParamsVpg, 0);
       if (i & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
     }
+#ifdef NERFHIP_EXP_PARAMS_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     __syncthreads();
   };
   for (int rb = 0; rb < n_blocks; rb += 2) {
@@ -3700,7 +3706,7 @@ int nerfhip_build_flags(void) {
     defined(NERFHIP_EXP_KS_MODES) || defined(NERFHIP_EXP_KS_SPLIT_F) ||                      \
     defined(NERFHIP_EXP_KS_SPLIT_H) || defined(NERFHIP_EXP_KS_VMWAIT) ||                     \
     defined(NERFHIP_EXP_KS_TRACE) || defined(NERFHIP_EXP_HOTBLOCK) ||                        \
-    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) ||                                                 \
+    defined(NERFHIP_EXP_SPLIT_AFTER_MFMA) || defined(NERFHIP_EXP_PARAMS_PRIO) ||             \
     defined(NERFHIP_EXP_NOBARRIER) || defined(NERFHIP_EXP_NOFLUSH) ||                        \
     defined(NERFHIP_EXP_NOSTAGE) || defined(NERFHIP_EXP_NO_FWDCOPY) ||                       \
     defined(NERFHIP_EXP_STAGE_IDENTITY) || defined(NERFHIP_EXP_X2PROXY) ||                   \
