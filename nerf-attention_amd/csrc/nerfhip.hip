@@ -2729,6 +2729,13 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
   gload(st1, 1);
   __syncthreads();
   PSTAMP(2);
+#ifdef NERFHIP_STAMPS
+  // slot 7: clock cycles (s_memtime) this wave spent from each block's last
+  // MFMA/split issue to leaving its barrier, summed (low 32 bits), and the
+  // whole block loop (high 32 bits)
+  uint64_t bwait = 0;
+  const uint64_t tloop = __builtin_amdgcn_s_memtime();
+#endif
   auto block = [&](int rb, f4 (&st_next)[NPT], f4 (&st_fill)[NPT]) {
     // st_next ← block rb+2 ; compute block rb ; LDS[(rb+1)&1] ← st_fill (block rb+1)
     gload(st_next, rb + 2 < n_blocks ? rb + 2 : n_blocks - 1);
@@ -2760,13 +2767,24 @@ __device__ __forceinline__ void dw_tile_x3(const KArgs& a, const float* __restri
 #ifdef NERFHIP_EXP_PARAMS_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
+#ifdef NERFHIP_STAMPS
+    const uint64_t tb = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#ifdef NERFHIP_STAMPS
+    bwait += __builtin_amdgcn_s_memtime() - tb;
+#endif
   };
   for (int rb = 0; rb < n_blocks; rb += 2) {
     block(rb, st0, st1);
     block(rb + 1, st1, st0);
   }
   PSTAMP(3);
+#ifdef NERFHIP_STAMPS
+  if (a.pstamps && (threadIdx.x & 63) == 0)
+    a.pstamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 7] =
+        (bwait & 0xffffffffull) | ((__builtin_amdgcn_s_memtime() - tloop) << 32);
+#endif
 
   // Adam on the wave's (TJ/2)×(TK/WK) part; lane holds rows (q&3)+8(q>>2)+4h, col lr.
   // The gradient is hi + lo.  The epilogue streams the (x, y) sub-tiles: the

@@ -5,7 +5,9 @@ sweep's heaviest W = 256 chunk: 40 deep fits), from a NERFHIP_STAMPS build:
   NERFHIP_LIB=build/variants/v_pstamps.so python tools/r6/pstamps_deep.py [epochs] [out.json]
 
 Per wave (s_memrealtime, 100 MHz): 0 entry, 1 first loads issued, 2 first block
-staged, 3 MFMA loop done, 4 epilogue issued; 5 HW_ID, 6 XCC_ID.  The last
+staged, 3 MFMA loop done, 4 epilogue issued; 5 HW_ID, 6 XCC_ID; 7 the block loop in s_memtime
+cycles (high 32 bits) and its barrier-side wait (low 32 bits: from each block's
+last MFMA/split issue through its barrier).  The last
 epoch's launch is kept.  Reports the workgroup durations of the heavy (MFMA)
 tiles, how many run at once over the launch per XCD, and the tail: the time
 after the last heavy workgroup STARTED, when the chip can only drain.
@@ -81,7 +83,22 @@ def main():
                           "last_start_us": round(float(start[(xcc == x) & heavy].max()), 2),
                           "peak_running": int(v.max())}
                       for x, v in sorted(per_x.items())}
-    res["cus_seen"] = int(len({(int(x), int(s), int(c)) for x, s, c in zip(xcc, se, cu)}))
+    # slot 7 (the block loop, s_memtime cycles): barrier-side wait summed over
+    # blocks (low 32 bits) and the whole loop (high 32 bits), every heavy wave
+    s7 = st[hv, :, 7].astype(np.uint64)
+    bw = (s7 & np.uint64(0xFFFFFFFF)).astype(np.float64)
+    lp = (s7 >> np.uint64(32)).astype(np.float64)
+    ok = lp > 0
+    if ok.any():
+        frac = bw[ok] / lp[ok]
+        loop_us = ((st[hv, :, 3] - st[hv, :, 2]) / 100.0)[ok]
+        res["block_loop"] = {
+            "barrier_wait_frac": {q: round(float(np.percentile(frac, p)), 3)
+                                  for q, p in (("p10", 10), ("p50", 50), ("p90", 90))},
+            "barrier_wait_frac_mean": round(float(frac.mean()), 3),
+            "loop_cycles_mean": round(float(lp[ok].mean()), 0),
+            "memtime_mhz": round(float((lp[ok] / np.maximum(loop_us, 1e-3)).mean()), 1)}
+    res["cus_seen"] =int(len({(int(x), int(s), int(c)) for x, s, c in zip(xcc, se, cu)}))
     # heavy workgroups that started in the first 5 µs vs later, and their durations
     first = hv[start[hv] < 5.0]
     later = hv[start[hv] >= 5.0]
