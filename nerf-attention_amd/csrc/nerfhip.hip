@@ -223,17 +223,39 @@ struct Flight {
 // Diagnostic build only (tools/stamps.py): per-wave s_memtime stamps at the
 // phase boundaries of the row kernel, written to a buffer nothing else reads.
 __device__ unsigned long long* g_stamps = nullptr;
+// The phase stamps go to a.pstamps + kRowStampsOff ([blocks][waves][16]): the
+// kernel arguments reach every translation unit, g_stamps only part 0's.
+constexpr size_t kRowStampsOff = 1u << 20;
 #define STAMP(k)                                                                       \
   do {                                                                                 \
-    if (g_stamps && a.mode == 0 && (threadIdx.x & 63) == 0)                            \
-      g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = \
+    if (a.pstamps && a.mode == 0 && (threadIdx.x & 63) == 0)                           \
+      a.pstamps[kRowStampsOff +                                                        \
+                ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = \
           __builtin_amdgcn_s_memtime();                                                \
   } while (0)
-// accumulate cycles into stamp slot k (8..15) of this wave
+// accumulate cycles into g_stamps slot k (8..11) of this wave (part 0's
+// kernels only, nerfhip_debug_set_stamps; a global
+// read-modify-write: it waits for the vector-memory ops in flight, so
+// NERFHIP_STAMPS_NOADD drops it where the phase totals and the clock matter)
+#ifndef NERFHIP_STAMPS_NOADD
 #define STAMP_ADD(k, v)                                                                \
   do {                                                                                 \
     if (g_stamps && (threadIdx.x & 63) == 0)                                           \
       g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] += (v); \
+  } while (0)
+#else
+#define STAMP_ADD(k, v) \
+  do {                  \
+  } while (0)
+#endif
+// s_memrealtime (100 MHz) into slot k (12, 13): the in-kernel clock is
+// Δs_memtime / Δs_memrealtime × 100 MHz
+#define STAMP_RT(k)                                                                    \
+  do {                                                                                 \
+    if (a.pstamps && a.mode == 0 && (threadIdx.x & 63) == 0)                           \
+      a.pstamps[kRowStampsOff +                                                        \
+                ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (k)] = \
+          __builtin_amdgcn_s_memrealtime();                                            \
   } while (0)
 #define MEMTIME() __builtin_amdgcn_s_memtime()
 // the 32-row kernel's stamps: [blocks][4 waves][32] from a.pstamps + 262144
@@ -280,6 +302,9 @@ __device__ unsigned long long* g_stamps = nullptr;
   } while (0)
 #define R32STAMP(p, k) \
   do {                 \
+  } while (0)
+#define STAMP_RT(k) \
+  do {             \
   } while (0)
 #define PSTAMP(k) \
   do {            \
@@ -1020,6 +1045,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   float* bias = lds + WBUF;   // a phase's bias, or w0 ‖ b0 in the layer-0 backward
   int fit, tile;
   if (!map_block(blockIdx.x, a.n_fits, a.n_pad / RowsCfg<W>::ROWS, fit, tile)) return;
+  STAMP_RT(12);
   STAMP(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1278,6 +1304,7 @@ __global__ void __launch_bounds__(RowsCfg<W>::THREADS, RowsCfg<W>::WAVES_PER_SIM
   };
   wide_layer(ic<1>, ic<0>, wsrc(true, 1), hb, no_pre, dz0_out, dz0_reduce);
   STAMP(5);
+  STAMP_RT(13);
 }
 
 // ---------------------------------------------------------------------------

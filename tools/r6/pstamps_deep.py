@@ -37,12 +37,15 @@ def main():
         sys.exit("not a NERFHIP_STAMPS library (set NERFHIP_LIB)")
     _plan, specs = sweep_280(2048, seed=0)
     sel = bench.heaviest_group(specs, 256, 0)
-    buf = torch.zeros(4096 * 4 * 8, dtype=torch.int64, device="cuda")
-    os.environ["NERFHIP_PSTAMPS"] = str(buf.data_ptr())
     job = engine.FitJob([specs[i] for i in sel], epochs, devices=[0])
+    # the parameter kernel's [4096][4][8] region, then the row kernel's stamps
+    # at kRowStampsOff = 2^20 ([blocks][waves][16]; tools/stamps.py reads them)
+    n_waves = sum(8 * ((g.n + 7) // 8) * (g.n_pad // 16) for g in job.groups)
+    buf = torch.zeros((1 << 20) + 16 * n_waves, dtype=torch.int64, device="cuda")
+    os.environ["NERFHIP_PSTAMPS"] = str(buf.data_ptr())   # read when the launch arguments are made
     job.launch()
     job.wait()
-    st = buf.view(-1, 4, 8).cpu().numpy().astype(np.int64)
+    st = buf[:4096 * 4 * 8].view(-1, 4, 8).cpu().numpy().astype(np.int64)
     used = st[:, 0, 0] > 0
     st = st[used]
     w0 = st[:, 0, :]                       # wave 0 of every workgroup
