@@ -954,7 +954,7 @@ __device__ __forceinline__ void gemm_phase_x3(const uint16_t* __restrict__ src, 
                           (hh == 0 && J >= 2 ? NST : 0);
     vm_wait_barrier(std::integral_constant<int, n_out>{});   // sub-chunk u+1 landed everywhere
 #endif
-#ifdef NERFHIP_STAMPS
+#if defined(NERFHIP_STAMPS) && !defined(NERFHIP_STAMPS_NOADD)
     asm volatile("s_waitcnt vmcnt(0)");
     const unsigned long long t_w1 = MEMTIME();
     STAMP_ADD(8, t_d1 - t_d0);     // DMA issue
